@@ -1,0 +1,220 @@
+"""Generate golden vectors from the reference's own routing code.  BUILD-CONTAINER ONLY.
+
+This script imports the reference's hot-path modules from ``/root/reference`` (read-only) with
+stub parent packages (``ddr`` itself needs Python >= 3.12 and hydra/xarray/pykan,
+none of which are installed; the three routing modules need only torch + SciPy).  It runs the
+reference ``MuskingumCunge`` forward + autograd backward on seeded inputs and writes small
+``.npz`` fixtures next to this file.  The reference never travels to the GPU box: only the
+fixtures do.
+
+Fixtures:
+  kat.npz       F1  reference KATs: general-diagonal solve + grads, hot-start chains, denormalize
+  sandbox.npz   F2  RAPID Sandbox 5-reach topology (10,20->30; 30,40->50), synthetic q', default p
+  tree300.npz   F3  300-reach random binary tree x 40 steps, learned n/q/p, loss = sum(W*out)
+  gauge.npz     F4  gauge mode (ragged outflow_idx incl. a negative index) + carry_state batch 2
+  c1.npz        F5  config C1 shape (2000 x 720): outlet series, sampled runoff, unit-param grads
+  csr.npz       F6  canonical CSR + PatternMapper (crow, col) for the F3 and F5 graphs
+
+Run:  python tests/golden/make_golden.py
+"""
+
+from __future__ import annotations
+
+import importlib.util
+import sys
+import types
+from pathlib import Path
+from types import SimpleNamespace
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+sys.path.insert(0, str(REPO))
+REF = Path("/root/reference/src/ddr")
+
+from ddr_amd import synthetic  # noqa: E402
+
+
+def load_reference():
+    def _load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[name] = m
+        spec.loader.exec_module(m)
+        return m
+
+    for pkg in ["ddr", "ddr.routing", "ddr.geometry", "ddr.validation"]:
+        m = types.ModuleType(pkg)
+        m.__path__ = []
+        sys.modules[pkg] = m
+    cfgmod = types.ModuleType("ddr.validation.configs")
+    cfgmod.Config = object
+    sys.modules["ddr.validation.configs"] = cfgmod
+    _load("ddr.geometry.trapezoidal", REF / "geometry/trapezoidal.py")
+    utils = _load("ddr.routing.utils", REF / "routing/utils.py")
+    mmc = _load("ddr.routing.mmc", REF / "routing/mmc.py")
+    return utils, mmc
+
+
+PARAMS_DEFAULT = dict(
+    parameter_ranges={"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]},
+    log_space_parameters=["p_spatial"],
+    defaults={"p_spatial": 21},
+    attribute_minimums={"discharge": 0.0001, "slope": 0.001, "velocity": 0.01, "depth": 0.01,
+                        "bottom_width": 0.01},
+)
+# tests/routing/test_utils.py:31-65 (mock config)
+PARAMS_MOCK = dict(
+    parameter_ranges={"n": [0.01, 0.1], "q_spatial": [0.1, 0.9], "p_spatial": [1.0, 200.0]},
+    log_space_parameters=["p_spatial"],
+    defaults={"p_spatial": 1.0},
+    attribute_minimums={"velocity": 0.1, "depth": 0.01, "discharge": 0.001, "bottom_width": 0.1,
+                        "slope": 0.001},
+)
+
+
+def cfg_of(params):
+    return SimpleNamespace(params=SimpleNamespace(**params))
+
+
+def routing_dc(n, rows, cols, attrs, outflow_idx=None, flow_scale=None):
+    a = sp.coo_matrix((np.ones(len(rows), dtype=np.float32), (rows, cols)), shape=(n, n)).tocsr()
+    adj = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)),
+                                  torch.from_numpy(a.indices.astype(np.int64)),
+                                  torch.from_numpy(a.data.astype(np.float32)), size=(n, n))
+    return SimpleNamespace(adjacency_matrix=adj, length=torch.from_numpy(attrs.length),
+                           slope=torch.from_numpy(attrs.slope), x=torch.from_numpy(attrs.x),
+                           top_width=torch.empty(0), side_slope=torch.empty(0), outflow_idx=outflow_idx,
+                           gage_catchment=None, observations=None, flow_scale=flow_scale)
+
+
+def run_ref(mmc, params, dc, qprime, u, W, carry_from=None):
+    mc = mmc.MuskingumCunge(cfg_of(params), device="cpu")
+    if carry_from is not None:
+        mc._discharge_t = carry_from
+    sp_params = {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in u.items()}
+    mc.setup_inputs(dc, torch.from_numpy(qprime), sp_params, carry_state=carry_from is not None)
+    out = mc.forward()
+    loss = (out * torch.from_numpy(W)).sum()
+    loss.backward()
+    grads = {f"grad_{k}": v.grad.numpy().copy() for k, v in sp_params.items()}
+    return dict(runoff=out.detach().numpy(), q_last=mc._discharge_t.detach().numpy(),
+                top_width=mc.top_width.detach().numpy(), side_slope=mc.side_slope.detach().numpy(),
+                **grads), mc
+
+
+def kat(utils, mmc):
+    out = {}
+    crow = torch.tensor([0, 1, 3, 5], dtype=torch.int32)
+    col = torch.tensor([0, 0, 1, 1, 2], dtype=torch.int32)
+    A = torch.tensor([2.0, 1.0, 3.0, 1.0, 4.0], requires_grad=True)
+    b = torch.tensor([2.0, 7.0, 13.0], requires_grad=True)
+    x = utils.triangular_sparse_solve(A, crow, col, b, True, False, "cpu")
+    x.sum().backward()
+    out.update(kat_crow=crow.numpy(), kat_col=col.numpy(), kat_A=A.detach().numpy(), kat_b=b.detach().numpy(),
+               kat_x=x.detach().numpy(), kat_gradA=A.grad.numpy(), kat_gradb=b.grad.numpy())
+    # hot start on linear chains (tests/routing/test_mmc.py:564-602)
+    for name, q in (("uniform5", np.full(5, 2.0, np.float32)), ("nonuniform4", np.array([3, 1, 2, 4], np.float32)),
+                    ("single", np.array([5.0], np.float32)), ("clamp3", np.full(3, 1e-5, np.float32))):
+        nn_ = len(q)
+        mc = mmc.MuskingumCunge(cfg_of(PARAMS_MOCK), device="cpu")
+        adj = torch.zeros(nn_, nn_)
+        for i in range(nn_ - 1):
+            adj[i + 1, i] = 1.0
+        mc.network = adj
+        mapper, _, _ = mc.create_pattern_mapper()
+        res = mmc.compute_hotstart_discharge(torch.from_numpy(q), mapper, mc.discharge_lb, "cpu")
+        out[f"hot_{name}_q"] = q
+        out[f"hot_{name}_out"] = res.numpy()
+    u = torch.tensor([0.0, 0.25, 0.5, 0.75, 1.0])
+    out["den_u"] = u.numpy()
+    out["den_lin"] = utils.denormalize(u, [0.015, 0.25]).numpy()
+    out["den_log"] = utils.denormalize(u, [1.0, 200.0], log_space=True).numpy()
+    return out
+
+
+def mapper_csr(mmc, n, rows, cols):
+    mc = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+    a = sp.coo_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(n, n)).tocsr()
+    mc.network = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)),
+                                         torch.from_numpy(a.indices.astype(np.int64)),
+                                         torch.from_numpy(a.data), size=(n, n))
+    mapper, _, _ = mc.create_pattern_mapper()
+    idx = (mapper.M_csr.to_dense().argmax(0)).numpy()
+    return a.indptr.astype(np.int64), a.indices.astype(np.int64), mapper.crow_indices.numpy(), \
+        mapper.col_indices.numpy(), idx
+
+
+def case(mmc, params, net, T, seed, outflow_idx=None, learn_p=True):
+    attrs = synthetic.reach_attributes(net.n, seed)
+    q = synthetic.lateral_inflow(net.n, T, seed)
+    u = synthetic.unit_parameters(net.n, seed)
+    if not learn_p:
+        u.pop("p_spatial")
+    G = net.n if outflow_idx is None else len(outflow_idx)
+    W = np.random.default_rng(seed + 4000).uniform(0, 1, (G, T)).astype(np.float32)
+    dc = routing_dc(net.n, net.rows, net.cols, attrs, outflow_idx)
+    res, mc = run_ref(mmc, params, dc, q, u, W)
+    inputs = dict(n=np.int64(net.n), rows=net.rows, cols=net.cols, length=attrs.length, slope=attrs.slope,
+                  x=attrs.x, qprime=q, W=W, **{f"u_{k}": v for k, v in u.items()})
+    return inputs, res, mc, dc
+
+
+def main():
+    torch.manual_seed(0)
+    utils, mmc = load_reference()
+    np.savez_compressed(HERE / "kat.npz", **kat(utils, mmc))
+
+    # F2 Sandbox: 10,20 -> 30 ; 30,40 -> 50 ; order [10, 20, 40, 30, 50] -> indices 0..4
+    rows = np.array([3, 3, 4, 4], np.int32)
+    cols = np.array([0, 1, 2, 3], np.int32)
+    net = synthetic.SyntheticNetwork(5, rows, cols, np.array([5]))
+    inputs, res, _, _ = case(mmc, PARAMS_MOCK, net, 80, 11, learn_p=False)
+    np.savez_compressed(HERE / "sandbox.npz", **inputs, **{f"ref_{k}": v for k, v in res.items()})
+
+    # F3 300-reach tree, learned p
+    net3 = synthetic.random_binary_tree(300, seed=3)
+    inputs, res, _, _ = case(mmc, PARAMS_DEFAULT, net3, 40, 3)
+    np.savez_compressed(HERE / "tree300.npz", **inputs, **{f"ref_{k}": v for k, v in res.items()})
+
+    # F4 gauge mode + carry_state
+    net4 = synthetic.random_binary_tree(60, seed=4)
+    outflow = [np.array([-1]), np.array([10, 20, 31]), np.array([45]), np.array([5, 59])]
+    inputs, res, mc, dc = case(mmc, PARAMS_DEFAULT, net4, 30, 4, outflow_idx=outflow)
+    q2 = synthetic.lateral_inflow(net4.n, 30, 4, t0=30)
+    u = {k: inputs[f"u_{k}"] for k in ("n", "q_spatial", "p_spatial")}
+    W2 = np.random.default_rng(99).uniform(0, 1, (len(outflow), 30)).astype(np.float32)
+    res2, _ = run_ref(mmc, PARAMS_DEFAULT, dc, q2, u, W2, carry_from=mc._discharge_t.detach().clone())
+    flat = np.concatenate(outflow)
+    offs = np.cumsum([0] + [len(o) for o in outflow])
+    np.savez_compressed(HERE / "gauge.npz", **inputs, outflow_flat=flat, outflow_offsets=offs,
+                        qprime2=q2, W2=W2, **{f"ref_{k}": v for k, v in res.items()},
+                        **{f"ref2_{k}": v for k, v in res2.items()})
+
+    # F5 C1 shape
+    net5 = synthetic.random_binary_tree(2000, seed=0)
+    inputs, res, _, _ = case(mmc, PARAMS_DEFAULT, net5, 720, 0)
+    sample = np.arange(0, 2000, 37)
+    qsum = np.float64(inputs["qprime"].astype(np.float64).sum())
+    small = {k: v for k, v in inputs.items() if k not in ("qprime", "W")}
+    np.savez_compressed(HERE / "c1.npz", **small, qprime_sum=qsum, W_seed=np.int64(4000), sample=sample,
+                        ref_runoff_sample=res["runoff"][sample], ref_outlet=res["runoff"][-1],
+                        ref_q_last=res["q_last"], ref_top_width=res["top_width"],
+                        ref_side_slope=res["side_slope"], ref_grad_n=res["grad_n"],
+                        ref_grad_q_spatial=res["grad_q_spatial"], ref_grad_p_spatial=res["grad_p_spatial"])
+
+    # F6 canonical CSR + PatternMapper layout
+    c3 = mapper_csr(mmc, 300, net3.rows, net3.cols)
+    c5 = mapper_csr(mmc, 2000, net5.rows, net5.cols)
+    np.savez_compressed(HERE / "csr.npz", t300_crow=c3[0], t300_col=c3[1], t300_mcrow=c3[2], t300_mcol=c3[3],
+                        t300_mapidx=c3[4], c1_crow=c5[0], c1_col=c5[1], c1_mcrow=c5[2], c1_mcol=c5[3],
+                        c1_mapidx=c5[4])
+    for f in sorted(HERE.glob("*.npz")):
+        print(f.name, f.stat().st_size)
+
+
+if __name__ == "__main__":
+    main()
