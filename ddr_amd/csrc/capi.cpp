@@ -1,0 +1,294 @@
+// C ABI of libddr_mc.so (include/ddr_mc.h).  No exception crosses this boundary; errors are
+// returned as ddr_status codes with a thread-local message (ddr_last_error).
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "internal.h"
+#include "route_args.h"
+
+namespace ddr {
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+ddr_status fail(ddr_status code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+const char* last_error_cstr() { return g_last_error.c_str(); }
+ddr_status hip_fail(hipError_t e, const char* where) {
+  g_last_error = std::string(where) + ": " + hipGetErrorString(e);
+  return DDR_ERR_HIP;
+}
+
+}  // namespace ddr
+
+
+using namespace ddr;
+
+namespace {
+
+template <typename R>
+ddr_status check_common(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, int64_t T) {
+  if (!gh || !c || !r) return fail(DDR_ERR_ARG, "null graph/consts/reaches");
+  if (T < 1) return fail(DDR_ERR_ARG, "T must be >= 1");
+  if (!r->n || !r->q_spatial || !r->p_spatial || !r->length || !r->slope || !r->x_storage)
+    return fail(DDR_ERR_ARG, "null per-reach input");
+  if (r->p_stride != 0 && r->p_stride != 1) return fail(DDR_ERR_ARG, "p_stride must be 0 or 1");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (T * (g->n + 1) > (int64_t(1) << 62)) return fail(DDR_ERR_ARG, "T * N overflows");
+  return DDR_OK;
+}
+
+template <typename R>
+void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r, int64_t T,
+                 const R* qprime, int32_t flags) {
+  std::memset(&a, 0, sizeof(a));
+  a.s = g->dev;
+  a.N = g->n;
+  a.T = T;
+  a.flags = flags;
+  a.p_stride = (int32_t)r->p_stride;
+  a.n = r->n;
+  a.q = r->q_spatial;
+  a.p = r->p_spatial;
+  a.L = r->length;
+  a.S = r->slope;
+  a.X = r->x_storage;
+  a.fs = r->flow_scale;
+  a.qprime = qprime;
+  a.c[0] = c->dt;
+  a.c[1] = c->discharge_lb;
+  a.c[2] = c->velocity_lb;
+  a.c[3] = c->velocity_ub;
+  a.c[4] = c->depth_lb;
+  a.c[5] = c->bottom_width_lb;
+  a.c[6] = c->side_slope_lb;
+  a.c[7] = c->side_slope_ub;
+}
+
+template <typename R>
+ddr_status check_resident(const Graph* g, bool backward) {
+  if (g->n_cut == 0) return DDR_OK;  // no inter-workgroup waits: any grid size is safe
+  const int cap = max_resident_blocks<R>(g, backward);
+  if (cap < 0) return fail(DDR_ERR_HIP, "occupancy query failed");
+  if ((int64_t)g->blocks.size() > cap)
+    return fail(DDR_ERR_CAPACITY, "schedule needs " + std::to_string(g->blocks.size()) +
+                                      " co-resident workgroups, device admits " + std::to_string(cap));
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, const R* qprime,
+                        int64_t T, const R* q0, R* runoff, R* x_save, double* bnd, void* status, R* q_last,
+                        R* tw, R* ss, int32_t flags, void* stream) {
+  ddr_status st = check_common<R>(gh, c, r, T);
+  if (st) return st;
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (!qprime) return fail(DDR_ERR_ARG, "null qprime");
+  if ((flags & DDR_FWD_CARRY) && !q0) return fail(DDR_ERR_ARG, "DDR_FWD_CARRY needs q0");
+  if ((flags & DDR_FWD_SAVE_X) && !x_save) return fail(DDR_ERR_ARG, "DDR_FWD_SAVE_X needs x_save");
+  if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: bnd buffer required");
+  if (!status) return fail(DDR_ERR_ARG, "null status block");
+  if ((st = check_resident<R>(g, false))) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
+  if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bnd, 0xFF, sizeof(double) * g->n_cut * T, s));
+  RouteArgs a;
+  fill_common<R>(a, g, c, r, T, qprime, flags);
+  a.q0 = q0;
+  a.runoff = runoff;
+  a.x_save = x_save;
+  a.bnd = bnd;
+  a.status = static_cast<unsigned*>(status);
+  a.q_last = q_last;
+  a.tw_last = tw;
+  a.ss_last = ss;
+  DDR_HIP(launch_route<R>(g, a, false, s));
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, const R* qprime,
+                         int64_t T, const R* x_save, const double* bnd, const R* grad, const ddr_gauges* gauges,
+                         double* bwd_bnd, void* status, R* gn, R* gq, R* gp, int32_t flags, void* stream) {
+  ddr_status st = check_common<R>(gh, c, r, T);
+  if (st) return st;
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (!qprime || !x_save || !grad || !gn || !gq || !gp || !status)
+    return fail(DDR_ERR_ARG, "null backward argument");
+  if (g->n_cut > 0 && (!bnd || !bwd_bnd)) return fail(DDR_ERR_ARG, "graph has cut edges: boundary buffers required");
+  if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
+    return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
+  if ((st = check_resident<R>(g, true))) return st;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
+  if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
+  RouteArgs a;
+  fill_common<R>(a, g, c, r, T, qprime, flags);
+  a.x_save = const_cast<R*>(x_save);
+  a.bnd = const_cast<double*>(bnd);
+  a.status = static_cast<unsigned*>(status);
+  a.grad_out = grad;
+  a.g_roff = gauges ? gauges->reach_offsets : nullptr;
+  a.g_rg = gauges ? gauges->reach_gauges : nullptr;
+  a.bwd_bnd = bwd_bnd;
+  a.gn = gn;
+  a.gq = gq;
+  a.gp = gp;
+  DDR_HIP(launch_route<R>(g, a, true, s));
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
+                      int32_t flags, R* out, void* stream) {
+  if (!gh || !x_save || !gz || !out || T < 1) return fail(DDR_ERR_ARG, "bad gauge_reduce arguments");
+  if (gz->n_gauges > 0 && (!gz->offsets || !gz->index)) return fail(DDR_ERR_ARG, "null gauge arrays");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  GaugeArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.s = g->dev;
+  a.T = T;
+  a.G = gz->n_gauges;
+  a.goff = gz->offsets;
+  a.gidx = gz->index;
+  a.pos_of_ref = g->dev.pos_of_ref;
+  a.block_of_pos = g->dev.block_of_pos;
+  a.qlb = qlb;
+  a.carry = (flags & DDR_FWD_CARRY) ? 1 : 0;
+  DDR_HIP(launch_gauge<R>(a, x_save, out, static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+
+}  // namespace
+
+#define DDR_GUARD(body)                                  \
+  try {                                                  \
+    body                                                 \
+  } catch (const std::exception& ex) {                   \
+    return fail(DDR_ERR_ARG, std::string("internal: ") + ex.what()); \
+  } catch (...) {                                        \
+    return fail(DDR_ERR_ARG, "internal error");          \
+  }
+
+extern "C" {
+
+ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols, const ddr_build_opts* opts,
+                           ddr_graph** out) {
+  DDR_GUARD({
+    if (!out) return fail(DDR_ERR_ARG, "null out");
+    Graph* g = nullptr;
+    ddr_status st = build_graph(n, e, rows, cols, opts, &g);
+    if (st) return st;
+    *out = reinterpret_cast<ddr_graph*>(g);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_destroy(ddr_graph* g) {
+  DDR_GUARD({
+    destroy_graph(reinterpret_cast<Graph*>(g));
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
+  if (!gh || !info) return fail(DDR_ERR_ARG, "null argument");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  info->n = g->n;
+  info->nnz = g->nnz;
+  info->n_basins = g->n_basins;
+  info->n_pieces = g->n_pieces;
+  info->n_blocks = (int64_t)g->blocks.size();
+  info->n_cut = g->n_cut;
+  info->max_depth = g->max_depth;
+  info->max_block_depth = g->max_block_depth;
+  info->reaches_per_thread = g->kr;
+  info->save_elems_per_t = g->n;
+  info->save_elems_fixed = g->sum_dn;
+  info->bnd_elems_per_t = g->n_cut;
+  info->bwd_elems_per_t = 2 * g->n_cut;
+  info->status_bytes = kStatusBytes;
+  return DDR_OK;
+}
+
+ddr_status ddr_graph_csr(const ddr_graph* gh, int64_t* crow, int64_t* col) {
+  if (!gh || !crow || (!col && reinterpret_cast<const Graph*>(gh)->nnz > 0)) return fail(DDR_ERR_ARG, "null argument");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  std::memcpy(crow, g->crow.data(), sizeof(int64_t) * (g->n + 1));
+  if (g->nnz) std::memcpy(col, g->col.data(), sizeof(int64_t) * g->nnz);
+  return DDR_OK;
+}
+
+ddr_status ddr_graph_structure(const ddr_graph* gh, int64_t* down, int64_t* dist, int64_t* basin, int64_t* block) {
+  if (!gh) return fail(DDR_ERR_ARG, "null graph");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  const size_t b = sizeof(int64_t) * g->n;
+  if (down) std::memcpy(down, g->down.data(), b);
+  if (dist) std::memcpy(dist, g->dist.data(), b);
+  if (basin) std::memcpy(basin, g->basin.data(), b);
+  if (block) std::memcpy(block, g->block_of.data(), b);
+  return DDR_OK;
+}
+
+ddr_status ddr_mc_forward_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                              const float* qprime, int64_t T, const float* q0, float* runoff, float* x_save,
+                              double* bnd, void* status, float* q_last, float* tw, float* ss, int32_t flags,
+                              void* stream) {
+  DDR_GUARD({ return forward_impl<float>(g, c, r, qprime, T, q0, runoff, x_save, bnd, status, q_last, tw, ss, flags, stream); })
+}
+ddr_status ddr_mc_forward_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                              const double* qprime, int64_t T, const double* q0, double* runoff, double* x_save,
+                              double* bnd, void* status, double* q_last, double* tw, double* ss, int32_t flags,
+                              void* stream) {
+  DDR_GUARD({ return forward_impl<double>(g, c, r, qprime, T, q0, runoff, x_save, bnd, status, q_last, tw, ss, flags, stream); })
+}
+ddr_status ddr_mc_backward_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                               const float* qprime, int64_t T, const float* x_save, const double* bnd,
+                               const float* grad, const ddr_gauges* gauges, double* bwd_bnd, void* status,
+                               float* gn, float* gq, float* gp, int32_t flags, void* stream) {
+  DDR_GUARD({ return backward_impl<float>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream); })
+}
+ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                               const double* qprime, int64_t T, const double* x_save, const double* bnd,
+                               const double* grad, const ddr_gauges* gauges, double* bwd_bnd, void* status,
+                               double* gn, double* gq, double* gp, int32_t flags, void* stream) {
+  DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream); })
+}
+ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T, const ddr_gauges* gz,
+                                double qlb, int32_t flags, float* out, void* stream) {
+  DDR_GUARD({ return gauge_impl<float>(g, x_save, T, gz, qlb, flags, out, stream); })
+}
+ddr_status ddr_gauge_reduce_f64(const ddr_graph* g, const double* x_save, int64_t T, const ddr_gauges* gz,
+                                double qlb, int32_t flags, double* out, void* stream) {
+  DDR_GUARD({ return gauge_impl<double>(g, x_save, T, gz, qlb, flags, out, stream); })
+}
+
+ddr_status ddr_graph_status(const void* status, void* stream) {
+  if (!status) return fail(DDR_ERR_ARG, "null status");
+  unsigned h[2] = {0, 0};
+  DDR_HIP(hipMemcpyAsync(h, status, sizeof(h), hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+  DDR_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  if (h[0]) return fail(DDR_ERR_TIMEOUT, std::to_string(h[0]) + " inter-workgroup hand-offs timed out (first block " +
+                                             std::to_string((int)h[1] - 1) + ")");
+  return DDR_OK;
+}
+
+ddr_status ddr_device_info(int32_t* n_cu, int32_t* max_resident) {
+  int dev = 0;
+  DDR_HIP(hipGetDevice(&dev));
+  hipDeviceProp_t prop;
+  DDR_HIP(hipGetDeviceProperties(&prop, dev));
+  if (n_cu) *n_cu = prop.multiProcessorCount;
+  if (max_resident) *max_resident = prop.multiProcessorCount;
+  return DDR_OK;
+}
+
+const char* ddr_last_error(void) { return ddr::last_error_cstr(); }
+const char* ddr_version(void) { return "ddr_mc 0.1.0 (gfx950)"; }
+
+}  // extern "C"

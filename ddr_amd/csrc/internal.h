@@ -1,0 +1,88 @@
+// Internal definitions shared by the host graph builder (graph.cpp), the routing kernels
+// (route.hip) and the C ABI (capi.cpp).  Not part of the public interface (include/ddr_mc.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ddr_mc.h"
+
+namespace ddr {
+
+// Reaches per thread of the routing kernels (template instantiations).
+constexpr int kBlockThreads = 512;
+constexpr int kMaxKR = 8;
+// Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").
+constexpr int kChunk = 32;
+
+// One workgroup's slice of the schedule.  Reaches of a block occupy internal positions
+// [pos0, pos0 + nloc); virtual inflows (edges from other blocks) [virt0, virt0 + nvirt).
+struct BlockDesc {
+  int32_t pos0;
+  int32_t nloc;
+  int32_t virt0;
+  int32_t nvirt;
+  int32_t cout0;   // index into cout_loc (reaches whose downstream lives in another block)
+  int32_t ncout;
+  int32_t dmax;    // ticks = T + dmax
+  int32_t pad;
+  int64_t pre_dn;  // sum over earlier blocks of dmax * nloc (x_save base = T*pos0 + pre_dn)
+};
+
+// Device-side schedule (structure of arrays, indexed by internal position unless noted).
+struct DevSchedule {
+  BlockDesc* blocks = nullptr;
+  int32_t* ref = nullptr;      // reference reach index
+  int32_t* off = nullptr;      // tick offset: step t of this reach runs at tick t + off
+  int32_t* upb = nullptr;      // first upstream entry in uplist
+  int32_t* upc = nullptr;      // number of upstream entries
+  int32_t* dloc = nullptr;     // downstream local index in the same block, -1 otherwise
+  int32_t* cut = nullptr;      // cut-edge id if the downstream is in another block, -1 otherwise
+  int32_t* uplist = nullptr;   // local index (< nloc) or nloc + virtual index
+  int32_t* v_edge = nullptr;   // per virtual: cut-edge id
+  int32_t* v_off = nullptr;    // per virtual: tick offset (= off(consumer) - 1)
+  int32_t* v_dloc = nullptr;   // per virtual: consumer local index
+  int32_t* cout_loc = nullptr; // per block list: local indices of reaches with cut >= 0
+  int32_t* pos_of_ref = nullptr;   // (N) internal position of each reference reach
+  int32_t* block_of_pos = nullptr; // (N) block of each internal position
+};
+
+struct Graph {
+  int64_t n = 0, nnz = 0;
+  std::vector<int64_t> crow, col;
+  std::vector<int64_t> down, dist, basin, block_of;
+  int64_t n_basins = 0, n_pieces = 0, n_cut = 0, max_depth = 0, max_block_depth = 0;
+  int bs = kBlockThreads, kr = 1;
+  int max_slots = 0;     // max over blocks of nloc + nvirt
+  int max_virt = 0, max_cout = 0;
+  int device = 0;
+  std::vector<BlockDesc> blocks;
+  int64_t sum_dn = 0;    // sum over blocks of dmax * nloc
+  DevSchedule dev;
+  std::vector<void*> allocations;
+};
+
+// error plumbing (capi.cpp)
+void set_error(const std::string& msg);
+ddr_status fail(ddr_status code, const std::string& msg);
+ddr_status hip_fail(hipError_t e, const char* where);
+const char* last_error_cstr();
+
+#define DDR_HIP(call)                                        \
+  do {                                                       \
+    hipError_t _e = (call);                                  \
+    if (_e != hipSuccess) return ::ddr::hip_fail(_e, #call); \
+  } while (0)
+
+// graph.cpp
+ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                       const ddr_build_opts* opts, Graph** out);
+void destroy_graph(Graph* g);
+
+// status block layout (device): word 0 = timeout count, word 1 = first failing block + 1
+constexpr int64_t kStatusBytes = 256;
+
+}  // namespace ddr

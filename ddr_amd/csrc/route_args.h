@@ -1,0 +1,61 @@
+// Kernel argument blocks and launchers shared by route.hip and capi.cpp.
+#pragma once
+
+#include "internal.h"
+
+namespace ddr {
+
+struct RouteArgs {
+  DevSchedule s;
+  int64_t N, T;
+  int32_t flags;
+  int32_t slot_stride;  // LDS slots per buffer (max nloc + nvirt over blocks)
+  int32_t ring_stride;  // doubles per virtual/cut-out import ring
+  int32_t p_stride;
+  const void* n;
+  const void* q;
+  const void* p;
+  const void* L;
+  const void* S;
+  const void* X;
+  const void* fs;
+  const void* qprime;
+  const void* q0;
+  void* runoff;
+  void* x_save;
+  double* bnd;
+  unsigned* status;
+  void* q_last;
+  void* tw_last;
+  void* ss_last;
+  // backward
+  const void* grad_out;
+  const int64_t* g_roff;
+  const int64_t* g_rg;
+  double* bwd_bnd;
+  void* gn;
+  void* gq;
+  void* gp;
+  double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
+};
+
+struct GaugeArgs {
+  DevSchedule s;
+  int64_t T;
+  int64_t G;
+  const int64_t* goff;
+  const int64_t* gidx;
+  const int32_t* pos_of_ref;  // internal position of each reference reach
+  const int32_t* block_of_pos;
+  double qlb;
+  int32_t carry;
+};
+
+template <typename R>
+hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipStream_t stream);
+template <typename R>
+int max_resident_blocks(const Graph* g, bool backward);
+template <typename R>
+hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t stream);
+
+}  // namespace ddr

@@ -1,0 +1,284 @@
+"""PyTorch custom ops over the HIP routing library (``torch.library`` ``ddrx::*``).
+
+``ddrx::mc_route``          fused forward over all T steps     (mmc.py:365-443 + 487-559)
+``ddrx::mc_route_backward`` reverse-time adjoint               (autograd of the above)
+
+``mc_route`` is registered with ``register_autograd`` so the denormalised parameters
+(``n``, ``q_spatial``, ``p_spatial``) receive gradients exactly where the reference's autograd
+delivers them; everything upstream (``denormalize``, the KAN) stays PyTorch.
+
+The op takes the graph as an integer id into a registry of live :class:`RiverGraph` objects, raw
+device pointers go to the C ABI, and all work is enqueued on ``torch.cuda.current_stream()``.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import weakref
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from .graph import RiverGraph
+
+_GRAPHS: "weakref.WeakValueDictionary[int, RiverGraph]" = weakref.WeakValueDictionary()
+_CHECK_STATUS = os.environ.get("DDR_CHECK_STATUS", "0") == "1"
+
+
+def register_graph(g: RiverGraph) -> int:
+    gid = id(g)
+    _GRAPHS[gid] = g
+    return gid
+
+
+def _graph(gid: int) -> RiverGraph:
+    g = _GRAPHS.get(gid)
+    if g is None:
+        raise RuntimeError("routing graph was garbage-collected before use")
+    return g
+
+
+@dataclass(frozen=True)
+class RouteConsts:
+    """Physical constants (mmc.py:192-208; trapezoidal.py:79; mmc.py:166)."""
+
+    dt: float = 3600.0
+    discharge_lb: float = 1e-4
+    velocity_lb: float = 0.01
+    velocity_ub: float = 15.0
+    depth_lb: float = 0.01
+    bottom_width_lb: float = 0.01
+    side_slope_lb: float = 0.5
+    side_slope_ub: float = 50.0
+
+    def as_list(self) -> list[float]:
+        return [self.dt, self.discharge_lb, self.velocity_lb, self.velocity_ub, self.depth_lb, self.bottom_width_lb,
+                self.side_slope_lb, self.side_slope_ub]
+
+
+def _consts(c: list[float]) -> _lib.Consts:
+    return _lib.Consts(*[float(v) for v in c])
+
+
+def _reaches(n, q, p, length, slope, x_storage, flow_scale) -> _lib.Reaches:
+    return _lib.Reaches(n.data_ptr(), q.data_ptr(), p.data_ptr(), 1 if p.numel() > 1 else 0, length.data_ptr(),
+                        slope.data_ptr(), x_storage.data_ptr(), flow_scale.data_ptr() if flow_scale is not None else None)
+
+
+def _gauges(G, g_off, g_idx, r_off, r_g) -> _lib.Gauges | None:
+    if g_off is None:
+        return None
+    return _lib.Gauges(G, g_off.data_ptr(), g_idx.data_ptr(), r_off.data_ptr() if r_off is not None else None,
+                       r_g.data_ptr() if r_g is not None else None)
+
+
+def _check_inputs(qprime, tensors):
+    if qprime.dim() != 2:
+        raise ValueError("streamflow must be (T, N)")
+    if not qprime.is_cuda:
+        raise RuntimeError("ddrx::mc_route runs on the HIP device only (no CPU fallback); move inputs to cuda")
+    dt = qprime.dtype
+    if dt not in (torch.float32, torch.float64):
+        raise TypeError("routing supports float32 and float64")
+    for t in tensors:
+        if t is not None and (t.dtype != dt or t.device != qprime.device or not t.is_contiguous()):
+            raise ValueError("all routing inputs must share dtype/device and be contiguous")
+
+
+@torch.library.custom_op("ddrx::mc_route", mutates_args=())
+def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Tensor, length: torch.Tensor,
+             slope: torch.Tensor, x_storage: torch.Tensor, flow_scale: torch.Tensor | None, q0: torch.Tensor | None,
+             g_off: torch.Tensor | None, g_idx: torch.Tensor | None, r_off: torch.Tensor | None,
+             r_g: torch.Tensor | None, graph_id: int, consts: list[float],
+             flags: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Returns (runoff, q_last, top_width_last, side_slope_last, x_save, bnd).
+
+    ``r_off``/``r_g`` (reach -> gauge map) are only consumed by the backward."""
+    _check_inputs(qprime, (n, q, p, length, slope, x_storage, flow_scale, q0))
+    g = _graph(graph_id)
+    T, N = qprime.shape
+    if N != g.n:
+        raise ValueError(f"streamflow has {N} reaches, network has {g.n}")
+    dev, dt = qprime.device, qprime.dtype
+    gauge = g_off is not None
+    G = g_off.numel() - 1 if gauge else N
+    save = bool(flags & _lib.DDR_FWD_SAVE_X) or gauge
+    fflags = flags | (_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_NO_RUNOFF if gauge else 0)
+    runoff = torch.empty((G, T), device=dev, dtype=dt)
+    x_save = torch.empty(g.save_numel(T) if save else 0, device=dev, dtype=dt)
+    bnd = torch.empty(g.bnd_numel(T), device=dev, dtype=torch.float64)
+    status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
+    q_last = torch.empty(N, device=dev, dtype=dt)
+    tw = torch.zeros(N, device=dev, dtype=dt)
+    ss = torch.zeros(N, device=dev, dtype=dt)
+    lib = _lib.load()
+    fwd = lib.ddr_mc_forward_f32 if dt == torch.float32 else lib.ddr_mc_forward_f64
+    stream = _lib.stream_ptr(dev)
+    r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
+    c = _consts(consts)
+    _lib.check(fwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, _lib.ptr(q0), runoff.data_ptr(),
+                   x_save.data_ptr() if save else None, bnd.data_ptr() if bnd.numel() else None, status.data_ptr(),
+                   q_last.data_ptr(), tw.data_ptr(), ss.data_ptr(), int(fflags), stream))
+    if gauge:
+        red = lib.ddr_gauge_reduce_f32 if dt == torch.float32 else lib.ddr_gauge_reduce_f64
+        gz = _gauges(G, g_off, g_idx, None, None)
+        _lib.check(red(g.handle, x_save.data_ptr(), T, C.byref(gz), float(consts[1]), int(fflags), runoff.data_ptr(),
+                       stream))
+    if _CHECK_STATUS:
+        _lib.check(lib.ddr_graph_status(status.data_ptr(), stream))
+    return runoff, q_last, tw, ss, x_save, bnd
+
+
+@mc_route.register_fake
+def _(qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, graph_id, consts, flags):
+    T, N = qprime.shape
+    G = g_off.shape[0] - 1 if g_off is not None else N
+    g = _graph(graph_id)
+    save = bool(flags & _lib.DDR_FWD_SAVE_X) or g_off is not None
+    return (qprime.new_empty((G, T)), qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N),
+            qprime.new_empty(g.save_numel(T) if save else 0), qprime.new_empty(g.bnd_numel(T), dtype=torch.float64))
+
+
+@torch.library.custom_op("ddrx::mc_route_backward", mutates_args=())
+def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor,
+                      p: torch.Tensor, length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor,
+                      flow_scale: torch.Tensor | None, x_save: torch.Tensor, bnd: torch.Tensor,
+                      r_off: torch.Tensor | None, r_g: torch.Tensor | None, graph_id: int, consts: list[float],
+                      flags: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial)."""
+    g = _graph(graph_id)
+    T, N = qprime.shape
+    dev, dt = qprime.device, qprime.dtype
+    grad_runoff = grad_runoff.to(dtype=dt).contiguous()
+    gn = torch.empty(N, device=dev, dtype=dt)
+    gq = torch.empty(N, device=dev, dtype=dt)
+    gp = torch.empty(N, device=dev, dtype=dt)
+    bwd_bnd = torch.empty(g.bwd_numel(T), device=dev, dtype=torch.float64)
+    status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
+    lib = _lib.load()
+    bwd = lib.ddr_mc_backward_f32 if dt == torch.float32 else lib.ddr_mc_backward_f64
+    stream = _lib.stream_ptr(dev)
+    r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
+    c = _consts(consts)
+    gz = None
+    if r_off is not None:
+        gz = _lib.Gauges(grad_runoff.shape[0], None, None, r_off.data_ptr(), r_g.data_ptr())
+    _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, x_save.data_ptr(),
+                   bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
+                   C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr() if bwd_bnd.numel() else None,
+                   status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), int(flags), stream))
+    if _CHECK_STATUS:
+        _lib.check(lib.ddr_graph_status(status.data_ptr(), stream))
+    return gn, gq, gp
+
+
+@mc_route_backward.register_fake
+def _(grad_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g, graph_id, consts,
+      flags):
+    N = qprime.shape[1]
+    return qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N)
+
+
+def _setup_context(ctx, inputs, output):
+    (qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, graph_id, consts,
+     flags) = inputs
+    runoff, q_last, tw, ss, x_save, bnd = output
+    ctx.graph_id = graph_id
+    ctx.consts = consts
+    ctx.flags = flags
+    ctx.gauge = g_off is not None
+    ctx.p_scalar = p.numel() == 1
+    ctx.p_shape = p.shape
+    ctx.save_for_backward(qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g)
+    ctx.set_materialize_grads(False)
+
+
+def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
+    qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g = ctx.saved_tensors
+    if g_tw is not None or g_ss is not None:
+        if (g_tw is not None and bool(g_tw.ne(0).any())) or (g_ss is not None and bool(g_ss.ne(0).any())):
+            raise NotImplementedError("gradients through top_width/side_slope are not supported by ddrx::mc_route")
+    T = qprime.shape[0]
+    if g_runoff is None:
+        g_runoff = torch.zeros((1 if ctx.gauge else qprime.shape[1], T), device=qprime.device, dtype=qprime.dtype)
+        if ctx.gauge:
+            raise NotImplementedError("gauge-mode backward needs a runoff gradient")
+    if g_qlast is not None:
+        if ctx.gauge:
+            if bool(g_qlast.ne(0).any()):
+                raise NotImplementedError("gradient through the final discharge state in gauge mode")
+        else:
+            # runoff[:, T-1] is the final state Q_{T-1}
+            g_runoff = g_runoff.clone()
+            g_runoff[:, T - 1] += g_qlast
+    gn, gq, gp = mc_route_backward(g_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd,
+                                   r_off, r_g, ctx.graph_id, ctx.consts, ctx.flags)
+    if ctx.p_scalar:
+        gp = gp.sum().reshape(ctx.p_shape)
+    return None, gn, gq, gp, None, None, None, None, None, None, None, None, None, None, None, None
+
+
+mc_route.register_autograd(_backward, setup_context=_setup_context)
+
+
+# -------------------------------------------------------------------------------------------------
+# Convenience wrapper used by the drop-in routing engine
+# -------------------------------------------------------------------------------------------------
+
+
+@dataclass
+class GaugeMap:
+    """outflow_idx (mmc.py:344-363) as device arrays in both directions."""
+
+    n_gauges: int
+    offsets: torch.Tensor
+    index: torch.Tensor
+    reach_offsets: torch.Tensor
+    reach_gauges: torch.Tensor
+
+    @classmethod
+    def build(cls, outflow_idx, n_reaches: int, device) -> "GaugeMap":
+        import numpy as np
+
+        idx = [np.asarray(i, dtype=np.int64).reshape(-1) for i in outflow_idx]
+        flat = np.concatenate(idx) if idx else np.zeros(0, dtype=np.int64)
+        if flat.size and (flat.max() >= n_reaches or flat.min() < -n_reaches):
+            raise AssertionError(f"Output index {flat.max()} out of bounds for discharge tensor of size {n_reaches}.")
+        flat = np.where(flat < 0, flat + n_reaches, flat)  # Python-style negative indices
+        offs = np.zeros(len(idx) + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([len(i) for i in idx])
+        gid = np.repeat(np.arange(len(idx), dtype=np.int64), [len(i) for i in idx])
+        order = np.argsort(flat, kind="stable")
+        roff = np.zeros(n_reaches + 1, dtype=np.int64)
+        np.add.at(roff, flat + 1, 1)
+        roff = np.cumsum(roff)
+        rg = gid[order]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        return cls(len(idx), t(offs), t(flat), t(roff), t(rg))
+
+
+def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Tensor,
+          length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor, *, flow_scale: torch.Tensor | None = None,
+          q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
+          save: bool | None = None):
+    """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last)."""
+    dt = qprime.dtype
+    dev = qprime.device
+
+    def prep(t):
+        return None if t is None else t.to(device=dev, dtype=dt).contiguous()
+
+    n, q, p, length, slope, x_storage, flow_scale, q0 = map(prep, (n, q, p, length, slope, x_storage, flow_scale, q0))
+    p = p.reshape(-1) if p.numel() > 1 else p.reshape(1)
+    if save is None:
+        save = torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
+    flags = (_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
+    gid = register_graph(graph)
+    gz = gauges
+    out = mc_route(qprime.contiguous(), n, q, p, length, slope, x_storage, flow_scale, q0,
+                   gz.offsets if gz else None, gz.index if gz else None, gz.reach_offsets if gz else None,
+                   gz.reach_gauges if gz else None, gid, consts.as_list(), flags)
+    runoff, q_last, tw, ss, _, _ = out
+    return runoff, q_last, tw, ss

@@ -1,0 +1,196 @@
+/*
+ * ddr_mc.h -- C ABI of the MI355X-native Muskingum-Cunge routing hot path (libddr_mc.so).
+ *
+ * This is the drop-in boundary for DDR's routing engine (taddyb/ddr, src/ddr/routing).  Every entry
+ * point takes plain pointers and sizes; device pointers are caller-allocated (e.g. by the PyTorch
+ * caching allocator) and never freed by the library.  All work is enqueued on the caller's stream.
+ * No C++ exception crosses this boundary: every call returns a ddr_status (0 = OK, < 0 = error)
+ * and ddr_last_error() returns a thread-local message.
+ *
+ * Reference interfaces each entry point replaces (file:line in /root/reference):
+ *   ddr_graph_build     src/ddr/geodatazoo/merit.py:197-223 (COO union -> scipy .tocsr())
+ *                       + src/ddr/routing/utils.py:25-163 (PatternMapper / get_network_idx)
+ *   ddr_graph_csr       scipy.sparse.coo_matrix(...).tocsr() canonical CSR (bit-exact target)
+ *   ddr_mc_forward      src/ddr/routing/mmc.py:365-443 (MuskingumCunge.forward) with
+ *                       mmc.py:487-559 (route_timestep), mmc.py:25-66 (compute_hotstart_discharge),
+ *                       mmc.py:102-168 + geometry/trapezoidal.py:14-108 (celerity),
+ *                       mmc.py:460-485 (coefficients), routing/utils.py:535-627 (solver forward)
+ *   ddr_mc_backward     torch autograd of the above + routing/utils.py:629-692 (solver backward,
+ *                       _backward_cpu 188-242 / _backward_gpu 245-310, _compute_A_gradients 321-389)
+ *   ddr_gauge_reduce    mmc.py:344-363, 405-411, 433-439 (ragged outflow_idx scatter_add)
+ *   ddr_tri_solve       routing/utils.py:695 triangular_sparse_solve (general CSR, non-unit diagonal)
+ *   ddr_tri_grad_values routing/utils.py:321-389 _compute_A_gradients (gradA = -gradb[row]*x[col])
+ */
+#ifndef DDR_MC_H
+#define DDR_MC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int ddr_status;
+enum {
+  DDR_OK = 0,
+  DDR_ERR_ARG = -1,           /* bad argument / shape                                  */
+  DDR_ERR_NOT_LOWER = -2,     /* adjacency not strictly lower triangular (unsorted)     */
+  DDR_ERR_NOT_DENDRITIC = -3, /* a reach drains into more than one downstream reach     */
+  DDR_ERR_DUPLICATE = -4,     /* duplicate edge (summed value != 1)                     */
+  DDR_ERR_HIP = -5,           /* HIP runtime error                                      */
+  DDR_ERR_CAPACITY = -6,      /* graph does not fit the co-resident grid of this device */
+  DDR_ERR_TIMEOUT = -7,       /* an inter-workgroup hand-off timed out (device status)  */
+  DDR_ERR_SINGULAR = -8       /* zero on the diagonal (ddr_tri_solve)                   */
+};
+
+/* Opaque river-graph handle: canonical CSR, dendritic down[] pointers, basin/piece partition and the
+ * per-workgroup schedule, uploaded to the current device.  Immutable after build: safe to share
+ * across host threads and streams on its device. */
+typedef struct ddr_graph ddr_graph;
+
+enum { DDR_BUILD_HOST_ONLY = 1 };
+
+typedef struct {
+  int32_t flags;              /* DDR_BUILD_HOST_ONLY: validate/partition, no upload  [in]  */
+  int32_t max_block_reaches;  /* cap on reaches per workgroup (0 = auto)             [in]  */
+  int32_t target_blocks;      /* desired workgroups (0 = auto: CU count)             [in]  */
+  int32_t max_resident;       /* co-resident workgroups of the device (0 = query)    [in]  */
+} ddr_build_opts;
+
+typedef struct {
+  int64_t n;              /* reaches                                                      */
+  int64_t nnz;            /* edges after canonicalisation                                  */
+  int64_t n_basins;       /* connected components (outlet basins)                          */
+  int64_t n_pieces;       /* schedulable pieces after splitting large basins               */
+  int64_t n_blocks;       /* workgroups of one routing launch                              */
+  int64_t n_cut;          /* inter-workgroup edges                                         */
+  int64_t max_depth;      /* longest reach-to-outlet path (hops + 1)                       */
+  int64_t max_block_depth;/* max over workgroups of the in-piece depth                    */
+  int64_t reaches_per_thread; /* KR of the routing kernel instantiation                   */
+  int64_t save_elems_per_t;   /* x_save elements = save_elems_per_t * T + save_elems_fixed  */
+  int64_t save_elems_fixed;
+  int64_t bnd_elems_per_t;    /* forward boundary buffer doubles = bnd_elems_per_t * T     */
+  int64_t bwd_elems_per_t;    /* backward boundary buffer doubles = bwd_elems_per_t * T    */
+  int64_t status_bytes;       /* device status word block (zeroed by the library)          */
+} ddr_graph_info;
+
+/* Build from a host COO (rows = downstream reach, cols = upstream reach, int32, E entries), the
+ * ddr-engine zarr contract (engine/src/ddr_engine/core/zarr_io.py:7-76).  Validates lower
+ * triangularity and dendritic structure, canonicalises (rows sorted, columns ascending), splits
+ * and packs basins into workgroups, and uploads the schedule to the current HIP device.
+ * Synchronous (the only host-synchronising call besides ddr_graph_status). */
+ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                           const ddr_build_opts* opts, ddr_graph** out);
+ddr_status ddr_graph_destroy(ddr_graph* g);
+ddr_status ddr_graph_get_info(const ddr_graph* g, ddr_graph_info* info);
+/* Canonical CSR of the adjacency into host buffers: crow (n+1), col (nnz), int64. */
+ddr_status ddr_graph_csr(const ddr_graph* g, int64_t* crow, int64_t* col);
+/* Host copies of the dendritic structure: down (n, -1 = outlet), dist (n, hops to outlet),
+ * basin (n, outlet reach id), block (n, workgroup id), each int64; any pointer may be NULL. */
+ddr_status ddr_graph_structure(const ddr_graph* g, int64_t* down, int64_t* dist, int64_t* basin,
+                               int64_t* block);
+
+/* Physical constants of the routing step (mmc.py:192-208, trapezoidal.py:79, mmc.py:166). */
+typedef struct {
+  double dt;             /* seconds per step (3600; BMI may override, ddr_bmi.py:208) */
+  double discharge_lb;   /* q_lb */
+  double velocity_lb;
+  double velocity_ub;    /* 15 */
+  double depth_lb;
+  double bottom_width_lb;
+  double side_slope_lb;  /* 0.5 */
+  double side_slope_ub;  /* 50 */
+} ddr_mc_consts;
+
+/* Per-reach inputs in the reference reach order.  Element type is float for the *_f32 entry
+ * points and double for the *_f64 ones.  p_spatial may be a single value (p_stride = 0). */
+typedef struct {
+  const void* n;           /* Manning n, denormalised                 (N)   */
+  const void* q_spatial;   /* Leopold & Maddock exponent, denormalised  (N)   */
+  const void* p_spatial;   /* Leopold & Maddock coefficient        (N) or (1) */
+  int64_t p_stride;        /* 1 (per reach) or 0 (scalar)                     */
+  const void* length;      /* m                                         (N)   */
+  const void* slope;       /* already clamped at the slope minimum     (N)   */
+  const void* x_storage;   /* Muskingum X                               (N)   */
+  const void* flow_scale;  /* optional per-reach q' multiplier (N) or NULL    */
+} ddr_mc_reaches;
+
+/* Gauge mode: out[g, t] = sum_{k in [off[g], off[g+1])} Q_t[idx[k]] (device int64 arrays,
+ * indices already normalised to [0, N)); reach_offsets/reach_gauges list, per reach, the gauges
+ * (with multiplicity) whose outflow set contains it. */
+typedef struct {
+  int64_t n_gauges;
+  const int64_t* offsets;        /* (G+1)                                         */
+  const int64_t* index;          /* (offsets[G]) reach ids                         */
+  const int64_t* reach_offsets;  /* (N+1) inverse map used by the backward        */
+  const int64_t* reach_gauges;   /* (offsets[G]) gauge id of each membership      */
+} ddr_gauges;
+
+enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4 };
+
+/* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
+ *   qprime     (T, N) lateral inflow, time-major, reference order
+ *   q0         (N) carried discharge (DDR_FWD_CARRY) or NULL
+ *   runoff     (N, T) (or (G, T) via ddr_gauge_reduce afterwards; pass DDR_FWD_NO_RUNOFF)
+ *   x_save     internal layout, see ddr_graph_info (DDR_FWD_SAVE_X), else may be NULL
+ *   bnd        forward boundary buffer (bnd_elems_per_t * T doubles; may be NULL if n_cut == 0);
+ *              must be kept unchanged for ddr_mc_backward
+ *   status     device status block (status_bytes)
+ *   q_last, top_width_last, side_slope_last (N), any may be NULL */
+ddr_status ddr_mc_forward_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                              const float* qprime, int64_t T, const float* q0, float* runoff,
+                              float* x_save, double* bnd, void* status, float* q_last,
+                              float* top_width_last, float* side_slope_last, int32_t flags,
+                              void* stream);
+ddr_status ddr_mc_forward_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                              const double* qprime, int64_t T, const double* q0, double* runoff,
+                              double* x_save, double* bnd, void* status, double* q_last,
+                              double* top_width_last, double* side_slope_last, int32_t flags,
+                              void* stream);
+
+/* Reverse-time, reverse-topological adjoint.  grad_runoff is (N, T), or (G, T) with gauges != NULL.
+ * Writes per-reach dL/dn, dL/dq_spatial, dL/dp_spatial (N each; for a scalar p the caller sums). */
+ddr_status ddr_mc_backward_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                               const float* qprime, int64_t T, const float* x_save,
+                               const double* bnd, const float* grad_runoff, const ddr_gauges* gauges,
+                               double* bwd_bnd, void* status, float* grad_n, float* grad_q,
+                               float* grad_p, int32_t flags, void* stream);
+ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                               const double* qprime, int64_t T, const double* x_save,
+                               const double* bnd, const double* grad_runoff, const ddr_gauges* gauges,
+                               double* bwd_bnd, void* status, double* grad_n, double* grad_q,
+                               double* grad_p, int32_t flags, void* stream);
+
+/* Gauge reduction of a forward's saved states (requires DDR_FWD_SAVE_X): runoff (G, T). */
+ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
+                                const ddr_gauges* gauges, double discharge_lb, int32_t flags,
+                                float* runoff, void* stream);
+ddr_status ddr_gauge_reduce_f64(const ddr_graph* g, const double* x_save, int64_t T,
+                                const ddr_gauges* gauges, double discharge_lb, int32_t flags,
+                                double* runoff, void* stream);
+
+/* Synchronise `stream` and read the device status block written by the last launches:
+ * returns DDR_OK or DDR_ERR_TIMEOUT. */
+ddr_status ddr_graph_status(const void* status, void* stream);
+
+/* General sparse triangular solve A x = b (lower) or A^T x = b (transpose = 1), CSR A with a
+ * non-unit diagonal, fp32 values accumulated in fp64 (SciPy semantics, utils.py:587-600).
+ * crow/col are HOST int64 arrays (the pattern); values, b, x are device float arrays.
+ * Synchronous w.r.t. the pattern upload only. */
+ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow_host, const int64_t* col_host,
+                         const float* values, const float* b, float* x, int32_t lower,
+                         int32_t transpose, void* stream);
+/* gradA[k] = -gradb[row(k)] * x[col(k)] for CSR (device int64 crow/col). */
+ddr_status ddr_tri_grad_values(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
+                               const float* gradb, const float* x, float* grad_values, void* stream);
+
+/* Device capacity helpers. */
+ddr_status ddr_device_info(int32_t* n_cu, int32_t* max_resident_blocks);
+const char* ddr_last_error(void);
+const char* ddr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DDR_MC_H */
