@@ -46,7 +46,7 @@ class GraphInfo(C.Structure):
     _fields_ = [(name, C.c_int64) for name in (
         "n", "nnz", "n_basins", "n_pieces", "n_blocks", "n_cut", "max_depth", "max_block_depth",
         "reaches_per_thread", "save_elems_per_t", "save_elems_fixed", "bnd_elems_per_t", "bwd_elems_per_t",
-        "status_bytes")]
+        "bwd_elems_fixed", "status_bytes")]
 
 
 class Consts(C.Structure):

@@ -120,13 +120,15 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   const Graph* g = reinterpret_cast<const Graph*>(gh);
   if (!qprime || !x_save || !grad || !gn || !gq || !gp || !status)
     return fail(DDR_ERR_ARG, "null backward argument");
-  if (g->n_cut > 0 && (!bnd || !bwd_bnd)) return fail(DDR_ERR_ARG, "graph has cut edges: boundary buffers required");
+  if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: forward boundary buffer required");
+  if (!bwd_bnd) return fail(DDR_ERR_ARG, "backward workspace required");
   if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
     return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
   if ((st = check_resident<R>(g, true))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
+  DDR_HIP(hipMemsetAsync(bwd_bnd + 2 * g->n_cut * T, 0, sizeof(double) * 3 * g->n, s));
   RouteArgs a;
   fill_common<R>(a, g, c, r, T, qprime, flags);
   a.x_save = const_cast<R*>(x_save);
@@ -212,6 +214,7 @@ ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
   info->save_elems_fixed = g->sum_dn;
   info->bnd_elems_per_t = g->n_cut;
   info->bwd_elems_per_t = 2 * g->n_cut;
+  info->bwd_elems_fixed = 3 * g->n;
   info->status_bytes = kStatusBytes;
   return DDR_OK;
 }

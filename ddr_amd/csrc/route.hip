@@ -10,6 +10,13 @@
 // are their own ready flag (sentinel = all ones, re-initialised before every launch), imported in
 // chunks of kChunk ticks so the hand-off latency is paid once per chunk.
 //
+// Each thread owns KR reaches (r = tid + k * 512).  Per tick the work is split in phases so that the
+// KR physics chains sit in one straight-line region the compiler can interleave:
+//   prefetch (global loads for the next tick, kept in a rotating register set)
+//   gather   (upstream sums from LDS; rare loop for >2 inflows)
+//   compute  (branch-free element-wise physics + fp64 column sweep, all KR reaches)
+//   publish  (LDS slots for the downstream reaches, predicated global stores)
+//
 // Reference semantics (file:line in /root/reference):
 //   forward  src/ddr/routing/mmc.py:365-443, 487-559, 25-66; routing/utils.py:587-600 (fp64 solve)
 //   backward routing/utils.py:629-692 + torch autograd of mmc.py/trapezoidal.py (hand adjoint)
@@ -69,13 +76,30 @@ __device__ __forceinline__ ReachStatic<R> load_static(const RouteArgs& a, int re
   return make_static<R>(n[ref], q[ref], p[(int64_t)ref * a.p_stride], S[ref], L[ref], X[ref]);
 }
 
-template <typename R>
-__device__ __forceinline__ R load_qprime(const RouteArgs& a, int64_t row, int ref) {
-  const R* qp = static_cast<const R*>(a.qprime);
-  R v = qp[row * a.N + ref];
-  if (a.fs) v = v * static_cast<const R*>(a.fs)[ref];  // mmc.py:303-304 (q' * flow_scale)
-  return v;
+// Packed upstream descriptor: u0 (13 bits) | u1 (13 bits) << 13 | min(nup, 15) << 26.
+__device__ __forceinline__ unsigned pack_up(const RouteArgs& a, int P) {
+  const int b = a.s.upb[P], c = a.s.upc[P];
+  const unsigned u0 = c > 0 ? (unsigned)a.s.uplist[b] : 0u;
+  const unsigned u1 = c > 1 ? (unsigned)a.s.uplist[b + 1] : 0u;
+  return u0 | (u1 << 13) | ((unsigned)(c < 15 ? c : 15) << 26);
 }
+// Make a per-reach value opaque inside the tick loop so the compiler recomputes what it derives
+// from it (64-bit addresses, qe + 1, ...) each tick instead of hoisting and keeping it live: at
+// KR reaches per thread the hoisted copies, not the state, exhaust the register file.
+template <typename V>
+__device__ __forceinline__ V opq(V x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+template <typename R>
+__device__ __forceinline__ ReachStatic<R> opq_static(ReachStatic<R> s) {
+  s.n = opq(s.n); s.qe = opq(s.qe); s.p = opq(s.p); s.sqrtS = opq(s.sqrtS); s.dd = opq(s.dd);
+  s.expo = opq(s.expo); s.inv_n = opq(s.inv_n); s.L = opq(s.L); s.X = opq(s.X);
+  return s;
+}
+__device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
+__device__ __forceinline__ int up_0(unsigned u) { return (int)(u & 8191u); }
+__device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u); }
 
 }  // namespace
 
@@ -83,28 +107,32 @@ __device__ __forceinline__ R load_qprime(const RouteArgs& a, int64_t row, int re
 // Forward
 // ============================================================================================
 template <typename R, int KR>
-__global__ void __launch_bounds__(kBlockThreads) route_forward_kernel(RouteArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sx = reinterpret_cast<double*>(smem);                 // [2][S]  x_j(t) (solve precision)
-  R* sq = reinterpret_cast<R*>(sx + 2 * S);                     // [2][S]  Q_j(t-1)
+  double* sx = reinterpret_cast<double*>(smem);  // [2][S]  x_j(t) (solve precision)
+  R* sq = reinterpret_cast<R*>(sx + 2 * S);      // [2][S]  Q_j(t-1)
   double* ring = reinterpret_cast<double*>(smem + ((2 * S * (8 + sizeof(R)) + 15) / 16) * 16);
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
+  const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool save = a.flags & DDR_FWD_SAVE_X;
   const bool write_runoff = !(a.flags & DDR_FWD_NO_RUNOFF) && a.runoff;
   R* runoff = static_cast<R*>(a.runoff);
   R* xsave = static_cast<R*>(a.x_save);
+  const R* qp = static_cast<const R*>(a.qprime);
+  const R* q0p = static_cast<const R*>(a.q0);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
 
   ReachStatic<R> st[KR];
-  int ref[KR], off[KR], upb[KR], upc[KR], cut[KR];
-  R Q[KR];
-  bool has[KR];
+  int ref[KR], off[KR];
+  unsigned up[KR];
+  bool has[KR], cut[KR];
+  R Q[KR], fsr[KR], qa[KR], qb[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -112,23 +140,40 @@ __global__ void __launch_bounds__(kBlockThreads) route_forward_kernel(RouteArgs 
     const int P = B.pos0 + (has[k] ? r : 0);
     ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
-    upb[k] = a.s.upb[P];
-    upc[k] = a.s.upc[P];
-    cut[k] = a.s.cut[P];
+    up[k] = pack_up(a, P);
+    cut[k] = a.s.cut[P] >= 0;
     st[k] = load_static<R>(a, ref[k]);
+    fsr[k] = a.fs ? static_cast<const R*>(a.fs)[ref[k]] : R(1);  // mmc.py:303-304 (q' * flow_scale)
     Q[k] = R(0);
+    qa[k] = qb[k] = R(0);
   }
-  // virtual inflows: thread v < nvirt owns virtual v
   const bool vown = tid < B.nvirt;
   int v_off = 0;
   R vQ = R(0);
-  if (vown) {
+  if (vown) v_off = a.s.v_off[B.virt0 + tid];
 
-    v_off = a.s.v_off[B.virt0 + tid];
-  }
-  const int TT = (int)T + B.dmax;
-  for (int tau = 0; tau < TT; ++tau) {
+  // q'[max(t-1,0)] (or the carried Q0 at t = 0) for the step each reach runs at tick `tau`
+  auto prefetch = [&](int tau, R(&dst)[KR]) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int tn = tau - off[k];
+      int64_t row = tn - 1;
+      row = row < 0 ? 0 : (row >= T ? T - 1 : row);
+      const R* src = (carry && tn == 0) ? (q0p + ref[k]) : (qp + row * N + ref[k]);
+      dst[k] = *src;
+    }
+  };
+
+  auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR]) {
     const int cur = tau & 1, prv = cur ^ 1;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      ref[k] = opq(ref[k]);
+      off[k] = opq(off[k]);
+      up[k] = opq(up[k]);
+      st[k] = opq_static(st[k]);
+      fsr[k] = opq(fsr[k]);
+    }
     if (B.nvirt > 0 && (tau % kChunk) == 0) {
       // import the next chunk of every virtual inflow into its ring half
       const int half = (tau / kChunk) & 1;
@@ -151,70 +196,84 @@ __global__ void __launch_bounds__(kBlockThreads) route_forward_kernel(RouteArgs 
         vQ = (t == 0 && carry) ? R(x) : rmax(R(x), cs.qlb);
       }
     }
+    prefetch(tau + 1, qnext);
+    // ---- one reach at a time: gather, physics, fp64 column sweep, publish ------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      if (!has[k]) continue;
       const int r = tid + k * BS;
-      const int64_t t = tau - off[k];
-      if (t < 0 || t >= T) continue;
-      const R Qprev = Q[k];
-      const int nup = upc[k];
-      double x;
-      R Qn;
-      if (t == 0) {
-        if (carry) {
-          x = (double)static_cast<const R*>(a.q0)[ref[k]];
-          Qn = R(x);
-        } else {
-          // hot start: (I - N) Q0 = q'[0] (mmc.py:25-66), fp64 column sweep, then clamp
-          double acc = (double)load_qprime<R>(a, 0, ref[k]);
-          for (int j = 0; j < nup; ++j) acc = acc + sx[prv * S + a.s.uplist[upb[k] + j]];
-          x = acc;
-          Qn = rmax(R(x), cs.qlb);
-        }
-      } else {
-        const R qc = rmax(load_qprime<R>(a, t - 1, ref[k]), cs.qlb);  // mmc.py:421-424
-        R c1, c2, c3, c4, tw, ss;
-        coefficients<R>(st[k], Qprev, cs, c1, c2, c3, c4, tw, ss);
-        R I = R(0);
-        for (int j = 0; j < nup; ++j) I = I + sq[prv * S + a.s.uplist[upb[k] + j]];  // N @ Q_t
-        const R b = ((c2 * I) + (c3 * Qprev)) + (c4 * qc);                           // mmc.py:538
-        double acc = (double)b;
-        const double dc1 = (double)c1;
-        for (int j = 0; j < nup; ++j) acc = acc + dc1 * sx[prv * S + a.s.uplist[upb[k] + j]];
-        x = acc;
-        Qn = rmax(R(x), cs.qlb);  // mmc.py:557
-        if (t == T - 1) {
-          if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = tw;
-          if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ss;
+      const int t = tau - off[k];
+      const int nup = up_n(up[k]);
+      // I = N @ Q_{t-1}, ascending column order (mmc.py:535)
+      const R q0v = sq[prv * S + up_0(up[k])];
+      const R q1v = sq[prv * S + up_1(up[k])];
+      const double x0v = sx[prv * S + up_0(up[k])];
+      const double x1v = sx[prv * S + up_1(up[k])];
+      R I = R(0);
+      I = I + (nup > 0 ? q0v : R(0));
+      I = I + (nup > 1 ? q1v : R(0));
+      if (nup > 2) {
+        const int P = B.pos0 + r;
+        const int b = a.s.upb[P], c = a.s.upc[P];
+        for (int j = 2; j < c; ++j) I = I + sq[prv * S + a.s.uplist[b + j]];
+      }
+      const R qv = qcur[k] * fsr[k];
+      R c1, c2, c3, c4, tw, ss;
+      coefficients<R>(st[k], Q[k], cs, c1, c2, c3, c4, tw, ss);
+      const R qc = rmax(qv, cs.qlb);                                  // mmc.py:421-424
+      const R b = ((c2 * I) + (c3 * Q[k])) + (c4 * qc);               // mmc.py:538
+      const double dc1 = (double)c1;
+      double acc = (double)b;                                         // utils.py:587-600 (fp64)
+      acc = acc + (nup > 0 ? dc1 * x0v : 0.0);
+      acc = acc + (nup > 1 ? dc1 * x1v : 0.0);
+      double hot = (double)qv;                                        // mmc.py:25-66 (hot start)
+      hot = hot + (nup > 0 ? x0v : 0.0);
+      hot = hot + (nup > 1 ? x1v : 0.0);
+      if (nup > 2) {
+        const int P = B.pos0 + r;
+        const int bb = a.s.upb[P], c = a.s.upc[P];
+        for (int j = 2; j < c; ++j) {
+          const double xj = sx[prv * S + a.s.uplist[bb + j]];
+          acc = acc + dc1 * xj;
+          hot = hot + xj;
         }
       }
-      sx[cur * S + r] = x;
-      sq[cur * S + r] = Qprev;
-      const R xr = R(x);
-      if (save) xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;
-      if (write_runoff) runoff[(int64_t)ref[k] * T + t] = (t == 0) ? rmax(xr, cs.qlb) : Qn;
-      if (cut[k] >= 0) store_granule(a.bnd + (int64_t)cut[k] * T + t, x);
-      if (t == T - 1 && a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
-      Q[k] = Qn;
+      if (has[k] && t >= 0 && t < T) {
+        const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
+        const R xr = R(x);
+        const R Qn = (t == 0 && carry) ? xr : rmax(xr, cs.qlb);        // mmc.py:557
+        sx[cur * S + r] = x;
+        sq[cur * S + r] = Q[k];
+        if (save) xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;
+        if (write_runoff) runoff[(int64_t)ref[k] * T + t] = (t == 0) ? rmax(xr, cs.qlb) : Qn;
+        if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
+        if (t == T - 1) {
+          if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
+          if (t > 0) {
+            if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = tw;
+            if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ss;
+          }
+        }
+        Q[k] = Qn;
+      }
+      // one reach's chain in flight: interleaving more spills registers at KR = 8
+      __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
+  };
+
+  const int TT = (int)T + B.dmax;
+  prefetch(0, qa);
+  for (int tau = 0; tau < TT; tau += 2) {
+    tick(tau, qa, qb);
+    if (tau + 1 < TT) tick(tau + 1, qb, qa);
   }
 }
 
 // ============================================================================================
 // Backward (adjoint)
 // ============================================================================================
-template <typename R>
-__device__ __forceinline__ R up_x(const RouteArgs& a, const BlockDesc& B, const R* xsave, int64_t xs_base,
-                                  int u, int tick, int64_t t) {
-  if (u < B.nloc) return xsave[xs_base + (int64_t)tick * B.nloc + u];
-  const int e = a.s.v_edge[B.virt0 + (u - B.nloc)];
-  return R(a.bnd[(int64_t)e * a.T + t]);
-}
-
 template <typename R, int KR>
-__global__ void __launch_bounds__(kBlockThreads) route_backward_kernel(RouteArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
@@ -225,16 +284,19 @@ __global__ void __launch_bounds__(kBlockThreads) route_backward_kernel(RouteArgs
   double* ring = reinterpret_cast<double*>(smem + ((2 * S * (8 + sizeof(R)) + 15) / 16) * 16);
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
+  const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const R* xsave = static_cast<const R*>(a.x_save);
   const R* gout = static_cast<const R*>(a.grad_out);
+  const R* qp = static_cast<const R*>(a.qprime);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
+  double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
 
   ReachStatic<R> st[KR];
-  int ref[KR], off[KR], upb[KR], upc[KR], dloc[KR], cut[KR], gb0[KR], gcnt[KR];
-  R lam[KR];
-  double acc_n[KR], acc_q[KR], acc_p[KR];
+  int ref[KR], off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
+  unsigned up[KR];
   bool has[KR];
+  R lam[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -242,31 +304,21 @@ __global__ void __launch_bounds__(kBlockThreads) route_backward_kernel(RouteArgs
     const int P = B.pos0 + (has[k] ? r : 0);
     ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
-    upb[k] = a.s.upb[P];
-    upc[k] = a.s.upc[P];
-    dloc[k] = a.s.dloc[P];
-    cut[k] = a.s.cut[P];
+    dl[k] = a.s.dloc[P];
+    up[k] = pack_up(a, P);
     st[k] = load_static<R>(a, ref[k]);
     lam[k] = R(0);
-    acc_n[k] = acc_q[k] = acc_p[k] = 0.0;
-    if (a.g_roff) {
-      gb0[k] = (int)a.g_roff[ref[k]];
-      gcnt[k] = (int)(a.g_roff[ref[k] + 1] - a.g_roff[ref[k]]);
-    } else {
-      gb0[k] = 0;
-      gcnt[k] = -1;
-    }
+    xa[k] = xb[k] = R(0);
+    pn[k] = pq[k] = pp[k] = R(0);
   }
-  // cut-out import ring slot: thread c < ncout owns cut-out reach cout_loc[c]
-  int my_cout_slot[KR];
-#pragma unroll
-  for (int k = 0; k < KR; ++k) my_cout_slot[k] = -1;
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
 #pragma unroll
     for (int k = 0; k < KR; ++k)
-      if (has[k] && tid + k * BS == loc) my_cout_slot[k] = c;
+      if (has[k] && tid + k * BS == loc) dl[k] = -(c + 2);
   }
+  const bool gauge = a.g_roff != nullptr;
+  const R* fs = static_cast<const R*>(a.fs);
   const bool vown = tid < B.nvirt;
   int v_edge = 0, v_off = 0, v_dloc = 0;
   if (vown) {
@@ -275,9 +327,35 @@ __global__ void __launch_bounds__(kBlockThreads) route_backward_kernel(RouteArgs
     v_dloc = a.s.v_dloc[B.virt0 + tid];
   }
   const int TT = (int)T + B.dmax;
-  for (int tb = 0; tb < TT; ++tb) {
+
+  // x of this reach at forward tick `tau` (clamped into the block's rows)
+  auto load_own = [&](int tau, R(&dst)[KR]) {
+    const int tc = tau < 0 ? 0 : (tau >= TT ? TT - 1 : tau);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + ((tid + k * BS) & (has[k] ? ~0 : 0))];
+  };
+  auto up_x = [&](int u, int tick, int64_t t) -> R {
+    if (u < B.nloc) {
+      const int tc = tick < 0 ? 0 : tick;
+      return xsave[xs_base + (int64_t)tc * B.nloc + u];
+    }
+    const int e = a.s.v_edge[B.virt0 + (u - B.nloc)];
+    const int64_t tt = t < 0 ? 0 : t;
+    return R(a.bnd[(int64_t)e * T + tt]);
+  };
+
+  // xp = x(t-1) of the step each reach runs at this tick; xn receives x(t-2) for the next tick
+  auto tick = [&](int tb, R(&xp)[KR], R(&xn)[KR]) {
     const int tau = TT - 1 - tb;  // forward tick
     const int cur = tb & 1, prv = cur ^ 1;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      ref[k] = opq(ref[k]);
+      off[k] = opq(off[k]);
+      up[k] = opq(up[k]);
+      dl[k] = opq(dl[k]);
+      st[k] = opq_static(st[k]);
+    }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
       const int half = (tb / kChunk) & 1;
       for (int w = tid; w < B.ncout * kChunk; w += BS) {
@@ -303,76 +381,119 @@ __global__ void __launch_bounds__(kBlockThreads) route_backward_kernel(RouteArgs
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[prv * S + v_dloc]);
       }
     }
+    load_own(tau - 2, xn);  // for the next tick
+    // ---- compute (one reach at a time; its loads are issued first and consumed after the
+    //      geometry recompute, which hides their latency) ------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      if (!has[k]) continue;
       const int r = tid + k * BS;
-      const int64_t t = tau - off[k];
-      if (t < 1 || t >= T) continue;
-      // dL/dQ_t += dL/dout[:, t]
-      R g;
-      if (gcnt[k] < 0) {
-        g = gout[(int64_t)ref[k] * T + t];
-      } else {
-        g = R(0);
-        for (int m = 0; m < gcnt[k]; ++m) g = g + gout[a.g_rg[gb0[k] + m] * T + t];
+      const int t = tau - off[k];
+      const bool active = has[k] && t >= 1 && t < T;
+      const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
+      R g[1], qv[1], xu[1][2], xup[1][2];
+      const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + (r & (has[k] ? ~0 : 0))];  // own x(t)
+      {
+        g[0] = gauge ? R(0) : gout[(int64_t)ref[k] * T + tcl];
+        const int64_t row = tcl >= 1 ? tcl - 1 : 0;
+        qv[0] = qp[row * N + ref[k]];
+        xu[0][0] = up_x(up_0(up[k]), tau - 1, tcl);
+        xu[0][1] = up_x(up_1(up[k]), tau - 1, tcl);
+        xup[0][0] = up_x(up_0(up[k]), tau - 2, tcl - 1);
+        xup[0][1] = up_x(up_1(up[k]), tau - 2, tcl - 1);
       }
-      lam[k] = lam[k] + g;
-      const R xt = xsave[xs_base + (int64_t)tau * B.nloc + r];
-      const R xp = xsave[xs_base + (int64_t)(tau - 1) * B.nloc + r];
-      const R gx = (xt >= cs.qlb) ? lam[k] : R(0);  // clamp backward (inclusive)
+      // downstream adjoint (c1_d gb_d, c2_d gb_d): LDS slot of the previous tick, or imported
       double A = 0.0;
       R Bd = R(0);
-      if (dloc[k] >= 0) {
-        A = sa[prv * S + dloc[k]];
-        Bd = sb[prv * S + dloc[k]];
-      } else if (my_cout_slot[k] >= 0) {
+      if (dl[k] >= 0) {
+        A = sa[prv * S + dl[k]];
+        Bd = sb[prv * S + dl[k]];
+      } else if (dl[k] <= -2) {
         const int sidx = (tb % (2 * kChunk));
-        A = ring[my_cout_slot[k] * a.ring_stride + sidx * 2];
-        Bd = R(ring[my_cout_slot[k] * a.ring_stride + sidx * 2 + 1]);
+        A = ring[(-dl[k] - 2) * a.ring_stride + sidx * 2];
+        Bd = R(ring[(-dl[k] - 2) * a.ring_stride + sidx * 2 + 1]);
       }
-      const double gb64 = (double)gx + A;  // (I - C1 N)^T gb = gx, fp64 (utils.py:188-242)
+      R gk = g[0];
+      if (gauge) {
+        const int64_t m0 = a.g_roff[ref[k]], m1 = a.g_roff[ref[k] + 1];
+        for (int64_t m = m0; m < m1; ++m) gk = gk + gout[a.g_rg[m] * T + tcl];
+      }
+      R qvk = qv[0];
+      if (fs) qvk = qvk * fs[ref[k]];                    // mmc.py:303-304
+      const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
+      const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
+      const double gb64 = (double)gx + A;                // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
       const R gb = R(gb64);
-      const R Qp = (t == 1 && carry) ? xp : rmax(xp, cs.qlb);
+      const R Qp = (t == 1 && carry) ? xp[k] : rmax(xp[k], cs.qlb);
       R c1, c2, c3, c4, tw, ss;
       Geom<R> geo;
       coefficients<R>(st[k], Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
-      R I = R(0), Sx = R(0);
-      const int nup = upc[k];
-      for (int j = 0; j < nup; ++j) {
-        const int u = a.s.uplist[upb[k] + j];
-        const R xu = up_x<R>(a, B, xsave, xs_base, u, tau - 1, t);
-        const R xu_p = up_x<R>(a, B, xsave, xs_base, u, tau - 2, t - 1);
-        Sx = Sx + xu;
-        I = I + ((t == 1 && carry) ? xu_p : rmax(xu_p, cs.qlb));
+      const int nup = up_n(up[k]);
+      R Sx = R(0), I = R(0);
+      const bool c0 = (t == 1 && carry);
+      Sx = Sx + (nup > 0 ? xu[0][0] : R(0));
+      Sx = Sx + (nup > 1 ? xu[0][1] : R(0));
+      I = I + (nup > 0 ? (c0 ? xup[0][0] : rmax(xup[0][0], cs.qlb)) : R(0));
+      I = I + (nup > 1 ? (c0 ? xup[0][1] : rmax(xup[0][1], cs.qlb)) : R(0));
+      if (nup > 2) {
+        const int P = B.pos0 + r;
+        const int b = a.s.upb[P], c = a.s.upc[P];
+        for (int j = 2; j < c; ++j) {
+          const int u = a.s.uplist[b + j];
+          Sx = Sx + up_x(u, tau - 1, t);
+          const R xj = up_x(u, tau - 2, t - 1);
+          I = I + (c0 ? xj : rmax(xj, cs.qlb));
+        }
       }
-      const R qc = rmax(load_qprime<R>(a, t - 1, ref[k]), cs.qlb);
+      const R qc = rmax(qvk, cs.qlb);
       const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
       R gQ, gn, gq, gp;
       coefficients_vjp<R>(st[k], Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
-      acc_n[k] += (double)gn;
-      acc_q[k] += (double)gq;
-      acc_p[k] += (double)gp;
-      sa[cur * S + r] = (double)c1 * gb64;
-      sb[cur * S + r] = c2 * gb;
-      lam[k] = ((gb * c3) + gQ) + Bd;
+      if (active) {
+        pn[k] = pn[k] + gn;
+        pq[k] = pq[k] + gq;
+        pp[k] = pp[k] + gp;
+        sa[cur * S + r] = (double)c1 * gb64;
+        sb[cur * S + r] = c2 * gb;
+        lam[k] = ((gb * c3) + gQ) + Bd;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // flush fp32 partial gradient sums into the fp64 accumulators once per chunk
+    if ((tb % kChunk) == kChunk - 1 || tb == TT - 1) {
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        if (!has[k]) continue;
+        double* g3 = gacc + (int64_t)ref[k] * 3;
+        atomicAdd(g3 + 0, (double)pn[k]);
+        atomicAdd(g3 + 1, (double)pq[k]);
+        atomicAdd(g3 + 2, (double)pp[k]);
+        pn[k] = pq[k] = pp[k] = R(0);
+      }
     }
     lds_barrier();
+  };
+
+  // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2
+  load_own(TT - 2, xa);
+  for (int tb = 0; tb < TT; tb += 2) {
+    tick(tb, xa, xb);
+    if (tb + 1 < TT) tick(tb + 1, xb, xa);
   }
-#pragma unroll
-  for (int k = 0; k < KR; ++k) {
-    if (!has[k]) continue;
-    static_cast<R*>(a.gn)[ref[k]] = R(acc_n[k]);
-    static_cast<R*>(a.gq)[ref[k]] = R(acc_q[k]);
-    static_cast<R*>(a.gp)[ref[k]] = R(acc_p[k]);
-  }
+}
+
+// Final fp64 accumulators -> R gradients (reference order).
+template <typename R>
+__global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq, R* gp) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  gn[i] = R(gacc[3 * i + 0]);
+  gq[i] = R(gacc[3 * i + 1]);
+  gp[i] = R(gacc[3 * i + 2]);
 }
 
 // ============================================================================================
 // Gauge reduction: out[g, t] = sum_{k} clamp(x_t[idx_k])  (mmc.py:405-411, 433-439)
 // ============================================================================================
-
-
 template <typename R>
 __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -409,20 +530,22 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   const size_t smem = route_smem_bytes<R>(g, backward);
   a.slot_stride = g->max_slots;
   a.ring_stride = backward ? 4 * kChunk : 2 * kChunk;
+  a.n_cut = g->n_cut;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
     auto kern = route_backward_kernel<R, KR>;
-    if (smem > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const unsigned fb = (unsigned)((g->n + 255) / 256);
+    hipLaunchKernelGGL(finish_grads_kernel<R>, dim3(fb), dim3(256), 0, stream, g->n,
+                       (const double*)(a.bwd_bnd + 2 * g->n_cut * a.T), (R*)a.gn, (R*)a.gq, (R*)a.gp);
   } else {
     auto kern = route_forward_kernel<R, KR>;
-    if (smem > 64 * 1024) {
-      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-      if (e != hipSuccess) return e;
-    }
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
   }
   return hipGetLastError();
@@ -434,7 +557,6 @@ hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipSt
     case 1: return launch_route_kr<R, 1>(g, a, backward, stream);
     case 2: return launch_route_kr<R, 2>(g, a, backward, stream);
     case 4: return launch_route_kr<R, 4>(g, a, backward, stream);
-    case 8: return launch_route_kr<R, 8>(g, a, backward, stream);
     default: return launch_route_kr<R, 8>(g, a, backward, stream);
   }
 }
@@ -444,18 +566,12 @@ int max_resident_blocks(const Graph* g, bool backward) {
   int nb = 0;
   const size_t smem = route_smem_bytes<R>(g, backward);
   const void* f = nullptr;
-#define DDR_PICK(KRV)                                                                   \
-  case KRV:                                                                             \
-    f = backward ? (const void*)route_backward_kernel<R, KRV> : (const void*)route_forward_kernel<R, KRV>; \
-    break;
   switch (g->kr) {
-    DDR_PICK(1)
-    DDR_PICK(2)
-    DDR_PICK(4)
-    default:
-      f = backward ? (const void*)route_backward_kernel<R, 8> : (const void*)route_forward_kernel<R, 8>;
+    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1>; break;
+    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2>; break;
+    case 4: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4>; break;
+    default: f = backward ? (const void*)route_backward_kernel<R, 8> : (const void*)route_forward_kernel<R, 8>;
   }
-#undef DDR_PICK
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) != hipSuccess) return -1;

@@ -8,6 +8,7 @@ namespace ddr {
 struct RouteArgs {
   DevSchedule s;
   int64_t N, T;
+  int64_t n_cut;
   int32_t flags;
   int32_t slot_stride;  // LDS slots per buffer (max nloc + nvirt over blocks)
   int32_t ring_stride;  // doubles per virtual/cut-out import ring

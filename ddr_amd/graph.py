@@ -33,6 +33,7 @@ class GraphInfo:
     save_elems_fixed: int
     bnd_elems_per_t: int
     bwd_elems_per_t: int
+    bwd_elems_fixed: int
     status_bytes: int
 
 
@@ -138,7 +139,7 @@ class RiverGraph:
         return self.info.bnd_elems_per_t * T
 
     def bwd_numel(self, T: int) -> int:
-        return self.info.bwd_elems_per_t * T
+        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:

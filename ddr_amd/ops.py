@@ -167,7 +167,7 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
         gz = _lib.Gauges(grad_runoff.shape[0], None, None, r_off.data_ptr(), r_g.data_ptr())
     _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, x_save.data_ptr(),
                    bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
-                   C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr() if bwd_bnd.numel() else None,
+                   C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(),
                    status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), int(flags), stream))
     if _CHECK_STATUS:
         _lib.check(lib.ddr_graph_status(status.data_ptr(), stream))

@@ -71,7 +71,8 @@ typedef struct {
   int64_t save_elems_per_t;   /* x_save elements = save_elems_per_t * T + save_elems_fixed  */
   int64_t save_elems_fixed;
   int64_t bnd_elems_per_t;    /* forward boundary buffer doubles = bnd_elems_per_t * T     */
-  int64_t bwd_elems_per_t;    /* backward boundary buffer doubles = bwd_elems_per_t * T    */
+  int64_t bwd_elems_per_t;    /* backward workspace doubles = bwd_elems_per_t * T          */
+  int64_t bwd_elems_fixed;    /*                            + bwd_elems_fixed              */
   int64_t status_bytes;       /* device status word block (zeroed by the library)          */
 } ddr_graph_info;
 

@@ -50,6 +50,7 @@ class Network:
     down: np.ndarray = field(init=False)  # (n,) int64, -1 for outlets
     height: np.ndarray = field(init=False)  # longest upstream path length (0 = headwater)
     dist: np.ndarray = field(init=False)  # hops to the basin outlet (0 = outlet)
+    solver: str = "levels"  # "levels" (vectorised sweep) or "scipy" (the reference recipe, for timing)
 
     def __post_init__(self) -> None:
         n = self.n
@@ -117,6 +118,8 @@ class Network:
         reference (``utils.py:587-600``): x_i = (b_i + c1_i*x_j1) + c1_i*x_j2 ... in ascending j.
         """
         c1 = c1.astype(np.float64)
+        if self.solver == "scipy":
+            return self._scipy_solve(c1, b, transpose=False)
         x = b.astype(np.float64).copy()
         for nodes, ups in self._up_levels:
             acc = x[nodes]
@@ -132,11 +135,36 @@ class Network:
         Dendritic form: y_j = g_j + c1_down(j) * y_down(j).
         """
         c1 = c1.astype(np.float64)
+        if self.solver == "scipy":
+            return self._scipy_solve(c1, g, transpose=True)
         y = g.astype(np.float64).copy()
         for nodes in self._down_levels[1:]:
             d = self.down[nodes]
             y[nodes] = y[nodes] + c1[d] * y[d]
         return y
+
+
+def _scipy_matrix(net: "Network", c1: np.ndarray):
+    import scipy.sparse as sp
+
+    rows = np.repeat(np.arange(net.n, dtype=np.int64), np.diff(net.crow))
+    r = np.concatenate([rows, np.arange(net.n)])
+    c = np.concatenate([net.col, np.arange(net.n)])
+    v = np.concatenate([-c1[rows].astype(np.float32).astype(np.float64), np.ones(net.n)])
+    return sp.csr_matrix((v, (r, c)), shape=(net.n, net.n))
+
+
+def _scipy_solve(self, c1, b, transpose):
+    """Reference recipe: SciPy spsolve_triangular on fp64 copies (utils.py:587-600, 188-242)."""
+    from scipy.sparse.linalg import spsolve_triangular
+
+    A = _scipy_matrix(self, c1)
+    if transpose:
+        return spsolve_triangular(A.T, np.asarray(b, np.float64), lower=False, unit_diagonal=False)
+    return spsolve_triangular(A, np.asarray(b, np.float64), lower=True, unit_diagonal=False)
+
+
+Network._scipy_solve = _scipy_solve
 
 
 def _levels_with_slots(crow, col, height):

@@ -67,7 +67,8 @@ def main():
                     print(name, kw, res, flush=True)
                 except Exception as e:  # noqa: BLE001
                     print(name, kw, dtype, "FAILED", repr(e), flush=True)
-                    raise
+                    if "co-resident" not in str(e):
+                        raise
 
 
 if __name__ == "__main__":
