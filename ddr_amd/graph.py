@@ -126,6 +126,29 @@ class RiverGraph:
         _lib.check(_lib.load().ddr_graph_csr(self._handle, crow.ctypes.data, col.ctypes.data))
         return crow, col[: self.info.nnz]
 
+    def pattern_mapper_layout(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(crow, col, src) of A = I + diag(d) N in the reference PatternMapper layout.
+
+        ``mmc.py:561-584`` + ``utils.py:65-87``: row i holds N's columns ascending, then the diagonal
+        (the largest column of a lower-triangular row); off-diagonal slots read ``datvec[i]``, the
+        diagonal slot ``datvec[0]``.
+        """
+        crow, col = self.csr()
+        n = self.n
+        deg = np.diff(crow)
+        crow_a = crow + np.arange(n + 1, dtype=np.int64)
+        nnz = int(crow_a[-1])
+        col_a = np.empty(nnz, dtype=np.int64)
+        src = np.empty(nnz, dtype=np.int64)
+        rows = np.repeat(np.arange(n, dtype=np.int64), deg)
+        pos_off = crow_a[:-1][rows] + (np.arange(len(col)) - crow[:-1][rows])
+        col_a[pos_off] = col
+        src[pos_off] = rows
+        diag_pos = crow_a[1:] - 1
+        col_a[diag_pos] = np.arange(n)
+        src[diag_pos] = 0
+        return crow_a, col_a, src
+
     def structure(self) -> dict[str, np.ndarray]:
         out = {k: np.zeros(self.n, dtype=np.int64) for k in ("down", "dist", "basin", "block")}
         _lib.check(_lib.load().ddr_graph_structure(self._handle, *(out[k].ctypes.data for k in

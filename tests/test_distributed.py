@@ -1,0 +1,120 @@
+"""World-size-2 (gloo, CPU) test of the multi-rank path: basin sharding + gradient all-reduce.
+
+Each rank routes only its outlet basins (oracle as the per-rank compute -- CPU test), back-propagates
+into a shared parameter network, and the all-reduced gradient equals the single-process gradient.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PARAMS_DEFAULT, synthetic_case
+
+T = 16
+
+
+def _problem():
+    from ddr_amd import synthetic
+
+    net = synthetic.forest(synthetic.loguniform_sizes(12, 20, 400, 1), seed=3)
+    case = synthetic_case(net, T, 3)
+    feats = np.random.default_rng(5).normal(size=(net.n, 4)).astype(np.float32)
+    return net, case, feats
+
+
+def _loss_grad(net_rows, net_cols, n, ids, case, feats, weight):
+    """dL/dweight for the reaches `ids` (loss = sum W * runoff, routed by the oracle)."""
+    from oracle import mc_oracle as O
+
+    w = torch.tensor(weight, requires_grad=True)
+    u = torch.sigmoid(torch.from_numpy(feats[ids]) @ w)  # (n_sub, 3): KAN-like parameter net
+    uu = u.detach().numpy().astype(np.float32)
+    rngs = PARAMS_DEFAULT["parameter_ranges"]
+    nn_ = O.denormalize(uu[:, 0], rngs["n"])
+    qq = O.denormalize(uu[:, 1], rngs["q_spatial"])
+    pp = O.denormalize(uu[:, 2], rngs["p_spatial"], True)
+    slope = np.maximum(case.slope[ids], np.float32(1e-3))
+    r = O.Reaches(nn_, qq, pp, case.length[ids], slope, case.x[ids])
+    net = O.Network.from_coo(n, net_rows, net_cols)
+    qp = case.qprime[:, ids]
+    res = O.route(net, r, qp, dtype=np.float64)
+    bw = O.route_backward(net, r, qp, res["x"], case.W[ids])
+    g = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], uu[:, 0], uu[:, 1], uu[:, 2], rngs)
+    gu = torch.from_numpy(np.stack([g["n"], g["q_spatial"], g["p_spatial"]], 1).astype(np.float32))
+    u.backward(gu)
+    return w.grad.numpy()
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from ddr_amd.distributed import allreduce_gradients, shard_network
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net, case, feats = _problem()
+    weight = np.random.default_rng(9).normal(size=(4, 3)).astype(np.float32) * 0.3
+    ns, rs, cs, ids = shard_network(net.n, net.rows, net.cols, rank, world)
+    p = torch.nn.Parameter(torch.zeros(4, 3))
+    p.grad = torch.from_numpy(_loss_grad(rs, cs, ns, ids, case, feats, weight))
+    allreduce_gradients([p])
+    n_local = torch.tensor([float(ns)])
+    dist.all_reduce(n_local)
+    out[rank] = (p.grad.numpy().copy(), float(n_local), ids)
+    dist.destroy_process_group()
+
+
+def test_two_rank_basin_sharding_and_grad_allreduce():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    world = 2
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    out = manager.dict()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    net, case, feats = _problem()
+    weight = np.random.default_rng(9).normal(size=(4, 3)).astype(np.float32) * 0.3
+    full = _loss_grad(net.rows, net.cols, net.n, np.arange(net.n), case, feats, weight)
+    g0, n0, ids0 = out[0]
+    g1, n1, ids1 = out[1]
+    assert n0 == n1 == net.n  # every reach routed exactly once
+    assert len(np.intersect1d(ids0, ids1)) == 0
+    np.testing.assert_allclose(g0, g1)
+    # fp32 sums over reaches in a different grouping: equal to summation-order rounding
+    np.testing.assert_allclose(g0, full, rtol=2e-4, atol=1e-5)
+
+
+def test_lpt_balance():
+    from ddr_amd.partition import lpt_assign, shard_basins
+
+    sizes = np.array([100, 90, 50, 40, 30, 20, 10, 5, 5, 1])
+    owner = lpt_assign(sizes, 3)
+    loads = np.bincount(owner, weights=sizes, minlength=3)
+    assert loads.max() - loads.min() <= sizes.max()
+    shards = shard_basins(sizes, 3)
+    assert sorted(np.concatenate(shards).tolist()) == list(range(len(sizes)))
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_shard_network_covers_every_reach(world):
+    from ddr_amd.distributed import shard_network
+
+    net, _, _ = _problem()
+    seen = []
+    for r in range(world):
+        ns, rs, cs, ids = shard_network(net.n, net.rows, net.cols, r, world)
+        assert ns == len(ids)
+        if len(rs):
+            assert np.all(rs > cs)  # still topologically ordered
+        seen.append(ids)
+    np.testing.assert_array_equal(np.sort(np.concatenate(seen)), np.arange(net.n))

@@ -1,0 +1,183 @@
+"""The drop-in ``dmc`` / ``MuskingumCunge`` / ``triangular_sparse_solve`` behave like the reference's
+(tests/routing/test_mmc.py, test_torch_mc.py, test_routing_utils.py), on the HIP path.
+"""
+
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PARAMS_DEFAULT, PARAMS_MOCK, cfg_of, golden_case, load_golden, maxrel, normrel
+from ddr_amd import synthetic
+from ddr_amd.routing import MuskingumCunge, compute_hotstart_discharge, dmc, triangular_sparse_solve
+
+pytestmark = pytest.mark.gpu
+
+
+def chain_dataclass(n, dev, seed=0, dense=True):
+    """tests/routing/test_utils.py:75-124 style mock (dense chain adjacency, outflow [-1])."""
+    g = torch.Generator().manual_seed(seed)
+    adj = torch.zeros(n, n)
+    for i in range(n - 1):
+        adj[i + 1, i] = 1.0
+    length = torch.clamp(torch.ones(n) * 1000.0 + torch.randn(n, generator=g) * 100, min=100.0)
+    slope = torch.clamp(torch.ones(n) * 0.001 + torch.randn(n, generator=g) * 1e-4, min=0.001)
+    return SimpleNamespace(adjacency_matrix=adj if dense else adj.to_sparse_csr(), length=length, slope=slope,
+                           x=torch.full((n,), 0.2), top_width=torch.empty(0), side_slope=torch.empty(0),
+                           outflow_idx=[np.array([-1])], gage_catchment=["wb-1"], observations=None,
+                           flow_scale=None)
+
+
+def golden_dataclass(case, outflow=None):
+    import scipy.sparse as sp
+
+    a = sp.coo_matrix((np.ones(len(case.rows), np.float32), (case.rows, case.cols)), shape=(case.n, case.n)).tocsr()
+    adj = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)), torch.from_numpy(a.indices.astype(np.int64)),
+                                  torch.from_numpy(a.data), size=(case.n, case.n))
+    return SimpleNamespace(adjacency_matrix=adj, length=torch.from_numpy(case.length), slope=torch.from_numpy(case.slope),
+                           x=torch.from_numpy(case.x), top_width=torch.empty(0), side_slope=torch.empty(0),
+                           outflow_idx=outflow, gage_catchment=None, observations=None, flow_scale=None)
+
+
+def test_dmc_matches_reference_golden(cuda):
+    case, d = golden_case("tree300", PARAMS_DEFAULT)
+    model = dmc(cfg_of(PARAMS_DEFAULT), device=cuda)
+    sp_params = {k: torch.from_numpy(v).to(cuda).requires_grad_(True) for k, v in case.u.items()}
+    out = model(routing_dataclass=golden_dataclass(case), streamflow=torch.from_numpy(case.qprime),
+                spatial_parameters=sp_params, retain_grads=True)["runoff"]
+    assert maxrel(out.detach().cpu().numpy(), d["ref_runoff"]) <= 1e-4
+    assert maxrel(model._discharge_t.detach().cpu().numpy(), d["ref_q_last"]) <= 1e-4
+    assert maxrel(model.top_width.detach().cpu().numpy(), d["ref_top_width"]) <= 1e-4
+    (out * torch.from_numpy(case.W).to(cuda)).sum().backward()
+    for k, v in sp_params.items():
+        assert normrel(v.grad.cpu().numpy(), d[f"ref_grad_{k}"]) <= 5e-5, k
+    assert model.n.grad is not None and out.grad is not None  # retain_grads (torch_mc.py:196-216)
+    assert len(list(model.parameters())) == 0
+
+
+def test_dmc_gauge_mode_sandbox_default_p(cuda):
+    case, d = golden_case("sandbox", PARAMS_MOCK)
+    model = dmc(cfg_of(PARAMS_MOCK), device=cuda)
+    sp_params = {k: torch.from_numpy(v).to(cuda).requires_grad_(True) for k, v in case.u.items() if v is not None}
+    out = model(routing_dataclass=golden_dataclass(case), streamflow=torch.from_numpy(case.qprime),
+                spatial_parameters=sp_params)["runoff"]
+    assert maxrel(out.detach().cpu().numpy(), d["ref_runoff"]) <= 1e-4
+    (out * torch.from_numpy(case.W).to(cuda)).sum().backward()
+    for k in ("n", "q_spatial"):
+        assert normrel(sp_params[k].grad.cpu().numpy(), d[f"ref_grad_{k}"]) <= 5e-5
+
+
+def test_mock_chain_gauge_output_shape_and_clamp(cuda):
+    """test_mmc.py:343-390: outflow_idx [-1] gives (1, T) output, values >= discharge_lb."""
+    mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    n, T = 10, 24
+    hf = chain_dataclass(n, cuda)
+    q = torch.clamp(5.0 + 2.0 * torch.sin(torch.linspace(0, 4 * np.pi, T))[:, None] + torch.zeros(T, n), min=0.1)
+    mc.setup_inputs(hf, q, {"n": torch.rand(n), "q_spatial": torch.rand(n)})
+    mc.set_progress_info(1, 0)
+    out = mc.forward()
+    assert out.shape == (1, T)
+    assert torch.isfinite(out).all() and (out >= mc.discharge_lb - 1e-6).all()
+    # gauge [-1] is the last reach: compare with full output
+    hf2 = chain_dataclass(n, cuda)
+    hf2.outflow_idx = None
+    mc2 = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    mc2.setup_inputs(hf2, q, mc.spatial_parameters)
+    full = mc2.forward()
+    torch.testing.assert_close(out[0], full[-1], rtol=0, atol=0)
+
+
+def test_hotstart_known_answers(cuda):
+    """tests/routing/test_mmc.py:564-602 on the device, through the mapper -> graph path."""
+    d = load_golden("kat")
+    for name in ("uniform5", "nonuniform4", "single", "clamp3"):
+        q = d[f"hot_{name}_q"]
+        n = len(q)
+        mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+        hf = chain_dataclass(n, cuda)
+        mc.setup_inputs(hf, torch.ones(12, n), {"n": torch.rand(n), "q_spatial": torch.rand(n)})
+        mapper, _, _ = mc.create_pattern_mapper()
+        res = compute_hotstart_discharge(torch.from_numpy(q).to(cuda), mapper, mc.discharge_lb, cuda)
+        np.testing.assert_array_equal(res.cpu().numpy(), d[f"hot_{name}_out"])
+
+
+def test_setup_inputs_semantics(cuda):
+    """Slope clamp, hot start, carry_state (test_mmc.py:83-99, 604-636)."""
+    mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    hf = chain_dataclass(5, cuda)
+    hf.slope = torch.tensor([0.00001, 0.001, 0.00005, 0.002, 0.00003])
+    mc.setup_inputs(hf, torch.ones(12, 5) * 2.0, {"n": torch.rand(5), "q_spatial": torch.rand(5)})
+    assert (mc.slope >= 0.001).all()
+    torch.testing.assert_close(mc._discharge_t.cpu(), torch.tensor([2.0, 4.0, 6.0, 8.0, 10.0]))
+    mc._discharge_t = torch.ones(5, device=cuda) * 99.0
+    mc.setup_inputs(hf, torch.ones(12, 5) * 2.0, {"n": torch.rand(5), "q_spatial": torch.rand(5)}, carry_state=True)
+    torch.testing.assert_close(mc._discharge_t.cpu(), torch.ones(5) * 99.0)
+    with pytest.raises(ValueError, match="routing_dataclass not set"):
+        MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda).forward()
+
+
+def test_route_timestep_matches_forward_step(cuda):
+    case, _ = golden_case("tree300", PARAMS_DEFAULT)
+    mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
+    hf = golden_dataclass(case)
+    sp_params = {k: torch.from_numpy(v).to(cuda) for k, v in case.u.items()}
+    qp = torch.from_numpy(case.qprime[:3]).to(cuda)
+    mc.setup_inputs(hf, qp, sp_params)
+    q0 = mc._discharge_t.clone()
+    full = mc.forward()
+    mc._discharge_t = q0
+    q1 = mc.route_timestep(torch.clamp(qp[0], min=1e-4), None)
+    torch.testing.assert_close(q1, full[:, 1], rtol=0, atol=0)
+
+
+def test_state_dict_roundtrip(cuda):
+    model = dmc(cfg_of(PARAMS_MOCK), device=cuda)
+    model.set_progress_info(3, 7)
+    sd = model.state_dict()
+    assert sd["epoch"] == 3 and sd["mini_batch"] == 7 and "cfg" in sd
+    m2 = dmc(cfg_of(PARAMS_MOCK), device=cuda)
+    m2.load_state_dict(sd)
+    assert m2.epoch == 3 and m2.mini_batch == 7 and m2.routing_engine.mini_batch == 7
+
+
+def test_triangular_solve_known_answer(cuda):
+    """tests/routing/test_routing_utils.py:132-166 + golden grads."""
+    d = load_golden("kat")
+    crow = torch.from_numpy(d["kat_crow"])
+    col = torch.from_numpy(d["kat_col"])
+    A = torch.from_numpy(d["kat_A"]).to(cuda).requires_grad_(True)
+    b = torch.from_numpy(d["kat_b"]).to(cuda).requires_grad_(True)
+    x = triangular_sparse_solve(A, crow, col, b, True, False, cuda)
+    np.testing.assert_array_equal(x.detach().cpu().numpy(), d["kat_x"])
+    x.sum().backward()
+    np.testing.assert_array_equal(A.grad.cpu().numpy(), d["kat_gradA"])
+    np.testing.assert_array_equal(b.grad.cpu().numpy(), d["kat_gradb"])
+    # identity system
+    n = 5
+    xi = triangular_sparse_solve(torch.ones(n, device=cuda), torch.arange(n + 1), torch.arange(n),
+                                 torch.arange(1.0, 6.0, device=cuda), True, False, cuda)
+    np.testing.assert_array_equal(xi.cpu().numpy(), np.arange(1.0, 6.0))
+    # zero diagonal -> ValueError like the reference (utils.py:598-600)
+    with pytest.raises(ValueError):
+        triangular_sparse_solve(torch.zeros(n, device=cuda), torch.arange(n + 1), torch.arange(n),
+                                torch.ones(n, device=cuda), True, False, cuda)
+
+
+def test_triangular_solve_routing_matrix(cuda):
+    """A = I - diag(c1) N from the mapper path equals the fp64 oracle sweep."""
+    from oracle import mc_oracle as O
+
+    net = synthetic.random_binary_tree(500, 2)
+    mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
+    hf = golden_dataclass(SimpleNamespace(n=net.n, rows=net.rows, cols=net.cols, length=np.ones(net.n, np.float32),
+                                          slope=np.ones(net.n, np.float32) * 1e-3, x=np.ones(net.n, np.float32) * .3))
+    mc.setup_inputs(hf, torch.ones(2, net.n), {"n": torch.rand(net.n), "q_spatial": torch.rand(net.n)})
+    mapper, _, _ = mc.create_pattern_mapper()
+    c1 = torch.rand(net.n, device=cuda) * 0.5
+    c1_ = c1 * -1
+    c1_[0] = 1.0
+    b = torch.rand(net.n, device=cuda)
+    x = triangular_sparse_solve(mapper.map(c1_), mapper.crow_indices, mapper.col_indices, b, True, False, cuda)
+    ref = O.Network.from_coo(net.n, net.rows, net.cols).lower_solve(c1.cpu().numpy(), b.cpu().numpy())
+    np.testing.assert_array_equal(x.cpu().numpy(), ref.astype(np.float32))

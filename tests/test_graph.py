@@ -1,0 +1,142 @@
+"""Graph construction (host side of ddr_graph_build): bit-exact CSR, dendritic structure, partition.
+
+Runs on CPU (DDR_BUILD_HOST_ONLY: validation + partition without device upload).
+Reference targets: scipy ``coo_matrix(...).tocsr()`` (merit.py:197-223) and the PatternMapper layout
+(utils.py:25-129, mmc.py:561-584) recorded in tests/golden/csr.npz.
+"""
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import load_golden
+from ddr_amd import _lib, synthetic
+from ddr_amd.graph import RiverGraph, adjacency_to_coo
+from oracle import mc_oracle as O
+
+
+def host_graph(n, rows, cols, **kw):
+    return RiverGraph(n, rows, cols, host_only=True, **kw)
+
+
+@pytest.mark.parametrize("net", [synthetic.random_binary_tree(2000, 0), synthetic.random_binary_tree(300, 3),
+                                 synthetic.forest(synthetic.zipf_sizes(20000, 200, 0.35), seed=1),
+                                 synthetic.hack_basin(5000, seed=2)], ids=["c1", "t300", "forest", "hack"])
+def test_csr_bit_exact_vs_scipy(net):
+    g = host_graph(net.n, net.rows, net.cols)
+    crow, col = g.csr()
+    a = sp.coo_matrix((np.ones(len(net.rows), np.float32), (net.rows, net.cols)), shape=(net.n, net.n)).tocsr()
+    np.testing.assert_array_equal(crow, a.indptr)
+    np.testing.assert_array_equal(col, a.indices)
+
+
+def test_csr_and_pattern_mapper_vs_reference_golden():
+    d = load_golden("csr")
+    for tag, net in (("t300", synthetic.random_binary_tree(300, 3)), ("c1", synthetic.random_binary_tree(2000, 0))):
+        g = host_graph(net.n, net.rows, net.cols)
+        crow, col = g.csr()
+        np.testing.assert_array_equal(crow, d[f"{tag}_crow"])
+        np.testing.assert_array_equal(col, d[f"{tag}_col"])
+        mcrow, mcol, src = g.pattern_mapper_layout()
+        np.testing.assert_array_equal(mcrow, d[f"{tag}_mcrow"])
+        np.testing.assert_array_equal(mcol, d[f"{tag}_mcol"])
+        np.testing.assert_array_equal(src, d[f"{tag}_mapidx"])
+
+
+def test_unsorted_coo_order_is_canonicalised():
+    net = synthetic.random_binary_tree(500, 1)
+    perm = np.random.default_rng(0).permutation(len(net.rows))
+    g1 = host_graph(net.n, net.rows, net.cols)
+    g2 = host_graph(net.n, net.rows[perm], net.cols[perm])
+    for a, b in zip(g1.csr(), g2.csr()):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_structure_matches_oracle():
+    net = synthetic.forest(synthetic.zipf_sizes(5000, 50, 0.35), seed=4)
+    g = host_graph(net.n, net.rows, net.cols)
+    s = g.structure()
+    o = O.Network.from_coo(net.n, net.rows, net.cols)
+    np.testing.assert_array_equal(s["down"], o.down)
+    np.testing.assert_array_equal(s["dist"], o.dist)
+    assert g.info.n_basins == len(net.basin_sizes)
+    assert g.info.max_depth == o.dist.max() + 1
+
+
+@pytest.mark.parametrize("rows,cols,code", [
+    ([0], [1], _lib.DDR_ERR_NOT_LOWER),          # upstream index above downstream: unsorted network
+    ([2, 2], [1, 1], _lib.DDR_ERR_DUPLICATE),    # duplicate edge
+    ([1, 2], [0, 0], _lib.DDR_ERR_NOT_DENDRITIC),  # reach 0 drains into two reaches
+    ([5], [0], _lib.DDR_ERR_ARG),                # index out of range
+    ([1], [1], _lib.DDR_ERR_NOT_LOWER),          # self loop
+])
+def test_invalid_networks_rejected(rows, cols, code):
+    with pytest.raises(_lib.DDRError) as e:
+        host_graph(3, np.array(rows), np.array(cols))
+    assert e.value.code == code
+    assert isinstance(e.value, ValueError)
+
+
+def test_empty_and_single_reach():
+    g = host_graph(1, np.zeros(0, np.int32), np.zeros(0, np.int32))
+    assert g.info.n_basins == 1 and g.info.n_blocks == 1 and g.info.max_depth == 1
+    crow, col = g.csr()
+    np.testing.assert_array_equal(crow, [0, 0])
+    assert col.size == 0
+    g = host_graph(4, np.zeros(0, np.int32), np.zeros(0, np.int32))  # isolated reaches
+    assert g.info.n_basins == 4
+
+
+@pytest.mark.parametrize("cap", [64, 200, 1024])
+def test_partition_invariants(cap):
+    net = synthetic.forest(synthetic.zipf_sizes(20000, 40, 0.5), seed=7, single_inflow=0.35)
+    g = host_graph(net.n, net.rows, net.cols, max_block_reaches=cap, target_blocks=1 << 20, max_resident=1 << 20)
+    s = g.structure()
+    blk = s["block"]
+    counts = np.bincount(blk)
+    assert counts.max() <= cap
+    assert g.info.n_blocks == len(counts) and counts.min() > 0
+    # cut edges = edges whose endpoints live in different blocks
+    cut = int(np.sum(blk[net.rows] != blk[net.cols]))
+    assert cut == g.info.n_cut
+    # block-level dependency graph must be acyclic (deadlock freedom of the persistent launch)
+    edges = {(int(a), int(b)) for a, b in zip(blk[net.cols], blk[net.rows]) if a != b}
+    indeg = np.zeros(len(counts), np.int64)
+    adj = [[] for _ in counts]
+    for a, b in edges:
+        adj[a].append(b)
+        indeg[b] += 1
+    stack = [i for i in range(len(counts)) if indeg[i] == 0]
+    seen = 0
+    while stack:
+        v = stack.pop()
+        seen += 1
+        for w in adj[v]:
+            indeg[w] -= 1
+            if indeg[w] == 0:
+                stack.append(w)
+    assert seen == len(counts), "block dependency graph has a cycle"
+    # save buffer sizes
+    assert g.save_numel(10) == net.n * 10 + g.info.save_elems_fixed
+
+
+def test_capacity_error_when_too_many_coresident_blocks():
+    net = synthetic.hack_basin(20000, seed=1)
+    with pytest.raises(_lib.DDRError) as e:
+        host_graph(net.n, net.rows, net.cols, max_block_reaches=64, max_resident=16)
+    assert e.value.code == _lib.DDR_ERR_CAPACITY
+
+
+def test_adjacency_layouts_agree():
+    import torch
+
+    net = synthetic.random_binary_tree(64, 5)
+    dense = net.dense()
+    ref = adjacency_to_coo(dense)
+    for adj in (torch.from_numpy(dense), torch.from_numpy(dense).to_sparse_csr(), torch.from_numpy(dense).to_sparse(),
+                sp.csr_matrix(dense)):
+        n, r, c = adjacency_to_coo(adj)
+        order = np.lexsort((c, r))
+        assert n == ref[0]
+        np.testing.assert_array_equal(r[order], ref[1])
+        np.testing.assert_array_equal(c[order], ref[2])

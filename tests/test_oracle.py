@@ -1,0 +1,112 @@
+"""The CPU oracle reproduces the reference's own outputs (golden vectors) -- pins the oracle.
+
+Tolerances: the oracle's fp32 path differs from the reference only through PyTorch's 1-ulp Sleef
+``powf`` (the oracle's pow is correctly rounded), measured <= 6e-7 max-rel on discharge; the hand
+adjoint (fp64) vs the reference's fp32 autograd is ~1e-5 norm-relative (the reference gradient's own
+fp32 noise: SURVEY §8(c)).
+"""
+
+import numpy as np
+import pytest
+
+from conftest import PARAMS_DEFAULT, PARAMS_MOCK, golden_case, load_golden, maxrel, normrel
+from oracle import mc_oracle as O
+
+FWD_TOL = 1e-5     # max relative error, discharge
+GRAD_TOL = 5e-5    # norm-relative error, parameter gradients
+
+
+def _grads(case, net, r, res_x, bd, outflow_idx=None, W=None):
+    bw = O.route_backward(net, r, case.qprime, res_x, case.W if W is None else W, bd, outflow_idx=outflow_idx)
+    return O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], case.u["n"], case.u["q_spatial"],
+                                   case.u.get("p_spatial"), case.params["parameter_ranges"])
+
+
+@pytest.mark.parametrize("name,params", [("sandbox", PARAMS_MOCK), ("tree300", PARAMS_DEFAULT), ("c1", PARAMS_DEFAULT)])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_oracle_matches_reference(name, params, dtype):
+    case, d = golden_case(name, params)
+    net, r, bd = case.network(), case.reaches(), case.bounds
+    res = O.route(net, r, case.qprime, bd, dtype=dtype)
+    if "ref_runoff" in d:
+        assert maxrel(res["runoff"], d["ref_runoff"]) < FWD_TOL
+    else:
+        assert maxrel(res["runoff"][d["sample"]], d["ref_runoff_sample"]) < FWD_TOL
+        assert maxrel(res["runoff"][-1], d["ref_outlet"]) < FWD_TOL
+    assert maxrel(res["q_last"], d["ref_q_last"]) < FWD_TOL
+    assert maxrel(res["top_width"], d["ref_top_width"]) < FWD_TOL
+    assert maxrel(res["side_slope"], d["ref_side_slope"]) < FWD_TOL
+    if name == "c1" and dtype == np.float32:
+        return  # one fp64 adjoint check at this size is enough for the CPU suite's time budget
+    res64 = res if dtype == np.float64 else O.route(net, r, case.qprime, bd, dtype=np.float64)
+    g = _grads(case, net, r, res64["x"], bd)
+    for k, v in g.items():
+        assert normrel(v, d[f"ref_grad_{k}"]) < GRAD_TOL, k
+
+
+def test_oracle_gauge_mode_and_carry_state():
+    case, d = golden_case("gauge", PARAMS_DEFAULT)
+    offs = d["outflow_offsets"]
+    outflow = [d["outflow_flat"][offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    net, r, bd = case.network(), case.reaches(), case.bounds
+    res = O.route(net, r, case.qprime, bd, outflow_idx=outflow)
+    assert res["runoff"].shape == d["ref_runoff"].shape
+    assert maxrel(res["runoff"], d["ref_runoff"]) < FWD_TOL
+    assert maxrel(res["q_last"], d["ref_q_last"]) < FWD_TOL
+    res64 = O.route(net, r, case.qprime, bd, dtype=np.float64, outflow_idx=outflow)
+    g = _grads(case, net, r, res64["x"], bd, outflow_idx=outflow)
+    for k, v in g.items():
+        assert normrel(v, d[f"ref_grad_{k}"]) < GRAD_TOL, k
+    # second batch continues from the carried state (mmc.py:330-333)
+    res2 = O.route(net, r, d["qprime2"], bd, q0=res["q_last"], outflow_idx=outflow)
+    assert maxrel(res2["runoff"], d["ref2_runoff"]) < FWD_TOL
+    res2_64 = O.route(net, r, d["qprime2"], bd, q0=res["q_last"], dtype=np.float64, outflow_idx=outflow)
+    bw = O.route_backward(net, r, d["qprime2"], res2_64["x"], d["W2"], bd, outflow_idx=outflow)
+    g2 = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], case.u["n"], case.u["q_spatial"],
+                                 case.u["p_spatial"], case.params["parameter_ranges"])
+    for k, v in g2.items():
+        assert normrel(v, d[f"ref2_grad_{k}"]) < GRAD_TOL, k
+
+
+def test_oracle_known_answers():
+    """Reference KATs (tests/routing/test_mmc.py:564-602, test_routing_utils.py:18-53)."""
+    d = load_golden("kat")
+    for name in ("uniform5", "nonuniform4", "single", "clamp3"):
+        q = d[f"hot_{name}_q"]
+        n = len(q)
+        net = O.Network.from_coo(n, np.arange(1, n), np.arange(0, n - 1))
+        out = O.hotstart(net, q, O.Bounds(discharge=0.001))
+        np.testing.assert_array_equal(out, d[f"hot_{name}_out"])
+    np.testing.assert_array_equal(O.hotstart(O.Network.from_coo(5, np.arange(1, 5), np.arange(4)),
+                                             np.full(5, 2.0, np.float32), O.Bounds()), [2, 4, 6, 8, 10])
+    np.testing.assert_array_equal(O.denormalize(d["den_u"], [0.015, 0.25]), d["den_lin"])
+    np.testing.assert_allclose(O.denormalize(d["den_u"], [1.0, 200.0], True), d["den_log"], rtol=2e-7)
+
+
+def test_coo_to_csr_matches_scipy():
+    import scipy.sparse as sp
+
+    rng = np.random.default_rng(0)
+    n = 500
+    rows = rng.integers(1, n, 3000)
+    cols = (rows * rng.uniform(0, 1, 3000)).astype(np.int64)
+    vals = rng.uniform(0, 1, 3000).astype(np.float32)
+    crow, col, v = O.coo_to_csr(n, rows, cols, vals)
+    a = sp.coo_matrix((vals, (rows, cols)), shape=(n, n)).tocsr()
+    np.testing.assert_array_equal(crow, a.indptr)
+    np.testing.assert_array_equal(col, a.indices)
+    np.testing.assert_allclose(v, a.data, rtol=1e-6)
+
+
+def test_scipy_recipe_equals_level_sweep():
+    from ddr_amd import synthetic
+
+    net = synthetic.forest(synthetic.zipf_sizes(3000, 20, 0.35), seed=2)
+    from conftest import synthetic_case
+
+    case = synthetic_case(net, 24, 2)
+    a, b = case.network(), case.network()
+    b.solver = "scipy"
+    r = case.reaches()
+    ra, rb = O.route(a, r, case.qprime), O.route(b, r, case.qprime)
+    np.testing.assert_array_equal(ra["runoff"], rb["runoff"])
