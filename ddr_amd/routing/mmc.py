@@ -24,22 +24,30 @@ from .utils import PatternMapper, denormalize, get_network_idx, triangular_spars
 
 log = logging.getLogger(__name__)
 
-_GRAPH_CACHE: "weakref.WeakKeyDictionary[Any, RiverGraph]" = weakref.WeakKeyDictionary()
+# id(adjacency) -> (weakref to the adjacency object, graph); identity-checked (tensors compare
+# element-wise, so they cannot be WeakKeyDictionary keys)
+_GRAPH_CACHE: dict[int, tuple[Any, RiverGraph]] = {}
 
 
 def graph_for(adjacency, device) -> RiverGraph:
     """Build (once per adjacency object) the device river graph of a RoutingDataclass adjacency."""
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    hit = _GRAPH_CACHE.get(id(adjacency))
+    if hit is not None:
+        ref, g = hit
+        if ref() is adjacency and g.device == dev:
+            return g
+    n, rows, cols = adjacency_to_coo(adjacency)
+    g = RiverGraph(n, rows, cols, device=dev)
     try:
-        g = _GRAPH_CACHE.get(adjacency)
+        ref = weakref.ref(adjacency)
     except TypeError:
-        g = None
-    if g is None or (g.device is not None and torch.device(device) != g.device):
-        n, rows, cols = adjacency_to_coo(adjacency)
-        g = RiverGraph(n, rows, cols, device=device)
-        try:
-            _GRAPH_CACHE[adjacency] = g
-        except TypeError:
-            pass
+        return g
+    for k in [k for k, (r, _) in _GRAPH_CACHE.items() if r() is None]:
+        del _GRAPH_CACHE[k]
+    _GRAPH_CACHE[id(adjacency)] = (ref, g)
     return g
 
 
