@@ -452,23 +452,21 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
         pn[k] = pn[k] + gn;
         pq[k] = pq[k] + gq;
         pp[k] = pp[k] + gp;
+        // flush the fp32 partial sums into the fp64 accumulators every kChunk *steps* (aligned to
+        // t, not to ticks, so the summation grouping -- and the result -- is independent of the
+        // partition); one owner per address, so the atomics are deterministic
+        if ((t % kChunk) == 1 || t == 1) {
+          double* g3 = gacc + (int64_t)ref[k] * 3;
+          atomicAdd(g3 + 0, (double)pn[k]);
+          atomicAdd(g3 + 1, (double)pq[k]);
+          atomicAdd(g3 + 2, (double)pp[k]);
+          pn[k] = pq[k] = pp[k] = R(0);
+        }
         sa[cur * S + r] = (double)c1 * gb64;
         sb[cur * S + r] = c2 * gb;
         lam[k] = ((gb * c3) + gQ) + Bd;
       }
       __builtin_amdgcn_sched_barrier(0);
-    }
-    // flush fp32 partial gradient sums into the fp64 accumulators once per chunk
-    if ((tb % kChunk) == kChunk - 1 || tb == TT - 1) {
-#pragma unroll
-      for (int k = 0; k < KR; ++k) {
-        if (!has[k]) continue;
-        double* g3 = gacc + (int64_t)ref[k] * 3;
-        atomicAdd(g3 + 0, (double)pn[k]);
-        atomicAdd(g3 + 1, (double)pq[k]);
-        atomicAdd(g3 + 2, (double)pp[k]);
-        pn[k] = pq[k] = pp[k] = R(0);
-      }
     }
     lds_barrier();
   };

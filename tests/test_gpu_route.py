@@ -138,7 +138,7 @@ def test_partition_invariance_and_determinism(cuda):
         assert alt["graph"].info.n_cut > 0
         np.testing.assert_array_equal(alt["runoff"], base["runoff"])
         for k in ("grad_n", "grad_q_spatial", "grad_p_spatial"):
-            np.testing.assert_allclose(alt[k], base[k], rtol=1e-6, atol=1e-12)
+            np.testing.assert_array_equal(alt[k], base[k])
 
 
 def test_basin_independence(cuda):
@@ -183,7 +183,7 @@ def test_finite_difference_gradient_fp64(cuda):
 def test_edge_cases(cuda):
     dev = cuda
     # single reach, T = 1 (hot start only), isolated reaches, a 4-inflow confluence
-    for n, rows, cols, T in ((1, [], [], 1), (1, [], [], 5), (6, [], [], 7), (6, [5, 5, 5, 5, 4], [0, 1, 2, 3, 4], 9)):
+    for n, rows, cols, T in ((1, [], [], 1), (1, [], [], 5), (6, [], [], 7), (6, [5, 5, 5, 5, 5], [0, 1, 2, 3, 4], 9)):
         net = synthetic.SyntheticNetwork(n, np.array(rows, np.int32), np.array(cols, np.int32), np.array([n]))
         case = synthetic_case(net, T, 3)
         res = run_hip(case, dev, dtype=torch.float64, grads=T > 1)
