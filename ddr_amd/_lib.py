@@ -17,7 +17,7 @@ from pathlib import Path
 
 import torch  # noqa: F401  (must precede the library load, see module docstring)
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libddr_mc.so"
+LIB_PATH = Path(os.environ.get("DDR_LIB") or Path(__file__).resolve().parent / "lib" / "libddr_mc.so")
 
 # status codes (include/ddr_mc.h)
 DDR_OK = 0

@@ -90,7 +90,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   const Graph* g = reinterpret_cast<const Graph*>(gh);
   if (!qprime) return fail(DDR_ERR_ARG, "null qprime");
   if ((flags & DDR_FWD_CARRY) && !q0) return fail(DDR_ERR_ARG, "DDR_FWD_CARRY needs q0");
-  if ((flags & DDR_FWD_SAVE_X) && !x_save) return fail(DDR_ERR_ARG, "DDR_FWD_SAVE_X needs x_save");
+  if (!x_save) return fail(DDR_ERR_ARG, "x_save is required (routing state, and the staging of runoff)");
   if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: bnd buffer required");
   if (!status) return fail(DDR_ERR_ARG, "null status block");
   if ((st = check_resident<R>(g, false))) return st;
@@ -108,6 +108,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   a.tw_last = tw;
   a.ss_last = ss;
   DDR_HIP(launch_route<R>(g, a, false, s));
+  if (runoff && !(flags & DDR_FWD_NO_RUNOFF)) DDR_HIP(launch_emit_runoff<R>(g, a, s));
   return DDR_OK;
 }
 
@@ -141,6 +142,9 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   a.gn = gn;
   a.gq = gq;
   a.gp = gp;
+  // workspace: [2 n_cut T f64 boundary][3 N f64 accumulators][grad in the schedule layout (R)]
+  a.gs = bwd_bnd + 2 * g->n_cut * T + 3 * g->n;
+  DDR_HIP(launch_expand_grad<R>(g, a, s));
   DDR_HIP(launch_route<R>(g, a, true, s));
   return DDR_OK;
 }

@@ -101,10 +101,10 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   g->device = dev;
   if (n_cu <= 0) n_cu = 256;
   const int bs = kBlockThreads;
-  int64_t hard_cap = int64_t(bs) * kMaxKR;
-  if (opts && opts->max_block_reaches > 0) hard_cap = std::min<int64_t>(hard_cap, opts->max_block_reaches);
-  int64_t target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu);
-  resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu;
+  int64_t hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, kDefaultBlockReaches);
+  if (opts && opts->max_block_reaches > 0) hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, opts->max_block_reaches);
+  int64_t target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu) * kBlocksPerCU;
+  resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
   int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + target - 1) / target));
 
   std::vector<int64_t> piece(n), resid(n), dloc_piece(n);
@@ -188,6 +188,31 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       block_of_piece[p] = best;
     }
     const int64_t nblocks = (int64_t)load.size();
+    {
+      // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if two
+      // workgroups would no longer fit on a CU
+      std::vector<int64_t> bv(nblocks, 0), bc(nblocks, 0);
+      for (size_t p = 0; p < pieces.size(); ++p) {
+        const int64_t d = g->down[pieces[p].root];
+        if (d >= 0) {
+          bv[block_of_piece[piece[d]]]++;
+          bc[block_of_piece[p]]++;
+        }
+      }
+      int64_t ms = 0, mv = 0, mc = 0;
+      for (int64_t b = 0; b < nblocks; ++b) {
+        ms = std::max(ms, load[b] + bv[b]);
+        mv = std::max(mv, bv[b]);
+        mc = std::max(mc, bc[b]);
+      }
+      const size_t need = std::max(route_lds_bytes(ms, mv, false, 4), route_lds_bytes(ms, mc, true, 4));
+      if (need > kLdsBudget) {
+        if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
+        hard_cap -= hard_cap / 8;
+        cap = std::min(cap, hard_cap);
+        continue;
+      }
+    }
     if (ncut > 0 && nblocks > resident) {
       if (cap >= hard_cap) {
         return fail(DDR_ERR_CAPACITY, "graph needs " + std::to_string(nblocks) +
@@ -308,6 +333,14 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     }
     if ((st = upload(g.get(), &D.pos_of_ref, pos_of_ref))) return st;
     if ((st = upload(g.get(), &D.block_of_pos, block_of_pos))) return st;
+    std::vector<int32_t> rtile;
+    for (int64_t b = 0; b < nblocks; ++b)
+      for (int32_t r0 = 0; r0 < g->blocks[b].nloc; r0 += kTileR) {
+        rtile.push_back((int32_t)b);
+        rtile.push_back(r0);
+      }
+    g->n_rtiles = (int64_t)rtile.size() / 2;
+    if ((st = upload(g.get(), &D.rtile, rtile))) return st;
     break;
   }
   *out = g.release();

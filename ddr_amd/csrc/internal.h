@@ -12,11 +12,31 @@
 
 namespace ddr {
 
-// Reaches per thread of the routing kernels (template instantiations).
+// Routing workgroups: 512 threads, up to kMaxKR reaches per thread, two workgroups per CU
+// (4 waves per SIMD: the per-reach statics live in LDS, not registers, so the 128-VGPR budget of
+// that occupancy holds KR = 4).
 constexpr int kBlockThreads = 512;
-constexpr int kMaxKR = 8;
+constexpr int kMaxKR = 4;
+constexpr int kBlocksPerCU = 2;
+// Default workgroup capacity (reaches): leaves LDS room for virtual inflows at two blocks per CU.
+constexpr int kDefaultBlockReaches = 1920;
+// LDS budget per workgroup for two per CU (160 KiB per CU).
+constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
 // Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").
 constexpr int kChunk = 32;
+// Transpose tiles between the (reach, step) layouts of the API and the tick-major schedule layout.
+constexpr int kTileR = 64;
+constexpr int kTileT = 64;
+
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+// Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
+// import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
+//   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64
+//   backward: A slots (f64) | B slots (R) | 6 statics (R) | ring [ncout][kChunk][2] f64
+__host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nring, bool backward, size_t rsize) {
+  const size_t base = backward ? slots * (8 + rsize + 6 * rsize) : slots * (8 + 6 * rsize);
+  return align16(base) + nring * kChunk * (backward ? 16 : 8);
+}
 
 // One workgroup's slice of the schedule.  Reaches of a block occupy internal positions
 // [pos0, pos0 + nloc); virtual inflows (edges from other blocks) [virt0, virt0 + nvirt).
@@ -48,6 +68,7 @@ struct DevSchedule {
   int32_t* cout_loc = nullptr; // per block list: local indices of reaches with cut >= 0
   int32_t* pos_of_ref = nullptr;   // (N) internal position of each reference reach
   int32_t* block_of_pos = nullptr; // (N) block of each internal position
+  int32_t* rtile = nullptr;        // (n_rtiles, 2) tiles of kTileR reaches: (block, first local index)
 };
 
 struct Graph {
@@ -61,6 +82,7 @@ struct Graph {
   int device = 0;
   std::vector<BlockDesc> blocks;
   int64_t sum_dn = 0;    // sum over blocks of dmax * nloc
+  int64_t n_rtiles = 0;  // tiles of kTileR reaches (never straddling a block) for the layout transposes
   DevSchedule dev;
   std::vector<void*> allocations;
 };

@@ -60,19 +60,27 @@ struct ReachStatic {
   __device__ __forceinline__ R omX() const { return R(1) - X; }
 };
 
+// The six stored fields (n, qe, p, sqrtS, L, X) -> the derived ones.  The routing kernels keep only
+// the stored fields (in LDS) and call this every tick; the operations are the same as at
+// construction, so the values are identical.
 template <typename R>
-__device__ __forceinline__ ReachStatic<R> make_static(R n, R q, R p, R S, R L, R X) {
+__device__ __forceinline__ ReachStatic<R> derive_static(R n, R qe, R p, R sqrtS, R L, R X) {
   ReachStatic<R> s;
   s.n = n;
-  s.qe = q + R(1e-6);
+  s.qe = qe;
   s.p = p;
-  s.sqrtS = rsqrt_(S);
-  s.dd = (p * s.sqrtS) + R(1e-8);
-  s.expo = dv(R(3), R(5) + R(3) * s.qe);
+  s.sqrtS = sqrtS;
+  s.dd = (p * sqrtS) + R(1e-8);
+  s.expo = dv(R(3), R(5) + R(3) * qe);
   s.inv_n = dv(R(1), n);
   s.L = L;
   s.X = X;
   return s;
+}
+
+template <typename R>
+__device__ __forceinline__ ReachStatic<R> make_static(R n, R q, R p, R S, R L, R X) {
+  return derive_static<R>(n, q + R(1e-6), p, rsqrt_(S), L, X);
 }
 
 // Forward intermediates kept for the VJP.

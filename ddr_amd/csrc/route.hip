@@ -4,18 +4,17 @@
 // One persistent workgroup owns a block of reaches (whole basins, or a connected piece of a large
 // basin) for the whole time window.  Reach i runs step t at tick t + off(i) with
 // off(i) = dmax - dist_in_piece(i): every upstream reach is exactly one tick ahead, so one
-// LDS double-buffer + one workgroup barrier per tick carries all in-block dependencies
+// LDS slot per reach + two workgroup barriers per tick carry all in-block dependencies
 // ("as late as possible" wavefront; T + dmax ticks instead of T x depth level syncs).
 // Edges between blocks (cut edges) are exchanged through global memory as 8-byte granules that
 // are their own ready flag (sentinel = all ones, re-initialised before every launch), imported in
 // chunks of kChunk ticks so the hand-off latency is paid once per chunk.
 //
-// Each thread owns KR reaches (r = tid + k * 512).  Per tick the work is split in phases so that the
-// KR physics chains sit in one straight-line region the compiler can interleave:
-//   prefetch (global loads for the next tick, kept in a rotating register set)
-//   gather   (upstream sums from LDS; rare loop for >2 inflows)
-//   compute  (branch-free element-wise physics + fp64 column sweep, all KR reaches)
-//   publish  (LDS slots for the downstream reaches, predicated global stores)
+// Each thread owns KR <= 4 reaches (r = tid + k * 512); two 512-thread workgroups share a CU
+// (4 waves per SIMD), so one workgroup's barrier wait is filled by the other's work.  The per-reach
+// statics live in LDS; registers hold only the per-reach state (Q, I, lambda, partial gradients)
+// and one tick of prefetched inputs.  Each tick: compute (reads upstream slots) -> barrier ->
+// publish (own slot) -> barrier.
 //
 // Reference semantics (file:line in /root/reference):
 //   forward  src/ddr/routing/mmc.py:365-443, 487-559, 25-66; routing/utils.py:587-600 (fp64 solve)
@@ -29,6 +28,7 @@ namespace ddr {
 namespace {
 
 constexpr unsigned long long kSentinel = ~0ull;
+
 
 __device__ __forceinline__ void lds_barrier() {
   // LDS hand-off only: global loads issued ahead (prefetch) stay in flight across the barrier.
@@ -91,48 +91,64 @@ __device__ __forceinline__ V opq(V x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-template <typename R>
-__device__ __forceinline__ ReachStatic<R> opq_static(ReachStatic<R> s) {
-  s.n = opq(s.n); s.qe = opq(s.qe); s.p = opq(s.p); s.sqrtS = opq(s.sqrtS); s.dd = opq(s.dd);
-  s.expo = opq(s.expo); s.inv_n = opq(s.inv_n); s.L = opq(s.L); s.X = opq(s.X);
-  return s;
-}
 __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
 __device__ __forceinline__ int up_0(unsigned u) { return (int)(u & 8191u); }
 __device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u); }
 
 }  // namespace
 
+// Per-reach statics in LDS: six arrays of S reals (n, qe, p, sqrtS, L, X).  The derived fields
+// (dd, expo, 1/n) are recomputed on every read (derive_static): 3 LDS reads and two divisions per
+// reach-step are cheaper than the ~9 registers per reach that holding them would cost.
+template <typename R>
+struct StatTab {
+  R* s;
+  int S;
+  __device__ __forceinline__ void put(int r, const ReachStatic<R>& v) const {
+    s[r] = v.n;
+    s[S + r] = v.qe;
+    s[2 * S + r] = v.p;
+    s[3 * S + r] = v.sqrtS;
+    s[4 * S + r] = v.L;
+    s[5 * S + r] = v.X;
+  }
+  __device__ __forceinline__ ReachStatic<R> get(int r) const {
+    return derive_static<R>(s[r], s[S + r], s[2 * S + r], s[3 * S + r], s[4 * S + r], s[5 * S + r]);
+  }
+};
+
 // ============================================================================================
 // Forward
 // ============================================================================================
+// Tick structure (one LDS slot per reach, single-buffered):
+//   [import a chunk of virtual inflows]  prefetch q' of the next tick
+//   compute: every reach reads its upstream x_j(t) from the slots (written last tick), runs the
+//            physics and the fp64 column sweep, keeps x in a register          -- barrier --
+//   publish: x into the reach's own slot (and virtual inflows into theirs)      -- barrier --
+// The inflow I(t+1) = sum_j Q_j(t) is formed from the same x_j(t) reads (Q_j = clamp(x_j)).
 template <typename R, int KR>
-__global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sx = reinterpret_cast<double*>(smem);  // [2][S]  x_j(t) (solve precision)
-  R* sq = reinterpret_cast<R*>(sx + 2 * S);      // [2][S]  Q_j(t-1)
-  double* ring = reinterpret_cast<double*>(smem + ((2 * S * (8 + sizeof(R)) + 15) / 16) * 16);
+  double* sx = reinterpret_cast<double*>(smem);                         // [S] x_j(t), solve precision
+  const StatTab<R> tab{reinterpret_cast<R*>(sx + S), S};                // [6][S]
+  double* ring = reinterpret_cast<double*>(smem + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
-  const bool save = a.flags & DDR_FWD_SAVE_X;
-  const bool write_runoff = !(a.flags & DDR_FWD_NO_RUNOFF) && a.runoff;
-  R* runoff = static_cast<R*>(a.runoff);
   R* xsave = static_cast<R*>(a.x_save);
   const R* qp = static_cast<const R*>(a.qprime);
   const R* q0p = static_cast<const R*>(a.q0);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
 
-  ReachStatic<R> st[KR];
   int ref[KR], off[KR];
   unsigned up[KR];
   bool has[KR], cut[KR];
-  R Q[KR], fsr[KR], qa[KR], qb[KR];
+  R Q[KR], In[KR], fsr[KR], qa[KR], qb[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -142,15 +158,15 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteAr
     off[k] = a.s.off[P];
     up[k] = pack_up(a, P);
     cut[k] = a.s.cut[P] >= 0;
-    st[k] = load_static<R>(a, ref[k]);
     fsr[k] = a.fs ? static_cast<const R*>(a.fs)[ref[k]] : R(1);  // mmc.py:303-304 (q' * flow_scale)
-    Q[k] = R(0);
+    Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
+    if (has[k]) tab.put(r, load_static<R>(a, ref[k]));
   }
   const bool vown = tid < B.nvirt;
   int v_off = 0;
-  R vQ = R(0);
   if (vown) v_off = a.s.v_off[B.virt0 + tid];
+  __syncthreads();
 
   // q'[max(t-1,0)] (or the carried Q0 at t = 0) for the step each reach runs at tick `tau`
   auto prefetch = [&](int tau, R(&dst)[KR]) {
@@ -165,62 +181,47 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteAr
   };
 
   auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR]) {
-    const int cur = tau & 1, prv = cur ^ 1;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       ref[k] = opq(ref[k]);
       off[k] = opq(off[k]);
       up[k] = opq(up[k]);
-      st[k] = opq_static(st[k]);
       fsr[k] = opq(fsr[k]);
     }
     if (B.nvirt > 0 && (tau % kChunk) == 0) {
-      // import the next chunk of every virtual inflow into its ring half
-      const int half = (tau / kChunk) & 1;
+      // import the next chunk of every virtual inflow (x of the upstream block's reach)
       for (int w = tid; w < B.nvirt * kChunk; w += BS) {
         const int v = w / kChunk, sidx = w % kChunk;
         const int e = a.s.v_edge[B.virt0 + v];
         const int t = tau + sidx - a.s.v_off[B.virt0 + v];
         double val = 0.0;
         if (t >= 0 && t < T) val = wait_granule(a.bnd + (int64_t)e * T + t, a.status);
-        ring[v * a.ring_stride + half * kChunk + sidx] = val;
+        ring[v * kChunk + sidx] = val;
       }
       lds_barrier();
     }
-    if (vown) {
-      const int t = tau - v_off;
-      if (t >= 0 && t < T) {
-        const double x = ring[tid * a.ring_stride + (tau % (2 * kChunk))];
-        sx[cur * S + B.nloc + tid] = x;
-        sq[cur * S + B.nloc + tid] = vQ;
-        vQ = (t == 0 && carry) ? R(x) : rmax(R(x), cs.qlb);
-      }
-    }
     prefetch(tau + 1, qnext);
-    // ---- one reach at a time: gather, physics, fp64 column sweep, publish ------------------
+    double xk[KR];
+    // ---- compute: one reach at a time (gather, physics, fp64 column sweep) -------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int r = tid + k * BS;
       const int t = tau - off[k];
       const int nup = up_n(up[k]);
-      // I = N @ Q_{t-1}, ascending column order (mmc.py:535)
-      const R q0v = sq[prv * S + up_0(up[k])];
-      const R q1v = sq[prv * S + up_1(up[k])];
-      const double x0v = sx[prv * S + up_0(up[k])];
-      const double x1v = sx[prv * S + up_1(up[k])];
-      R I = R(0);
-      I = I + (nup > 0 ? q0v : R(0));
-      I = I + (nup > 1 ? q1v : R(0));
-      if (nup > 2) {
-        const int P = B.pos0 + r;
-        const int b = a.s.upb[P], c = a.s.upc[P];
-        for (int j = 2; j < c; ++j) I = I + sq[prv * S + a.s.uplist[b + j]];
-      }
+      const ReachStatic<R> st = tab.get(has[k] ? r : 0);
       const R qv = qcur[k] * fsr[k];
       R c1, c2, c3, c4, tw, ss;
-      coefficients<R>(st[k], Q[k], cs, c1, c2, c3, c4, tw, ss);
+      coefficients<R>(st, Q[k], cs, c1, c2, c3, c4, tw, ss);
       const R qc = rmax(qv, cs.qlb);                                  // mmc.py:421-424
-      const R b = ((c2 * I) + (c3 * Q[k])) + (c4 * qc);               // mmc.py:538
+      const R b = ((c2 * In[k]) + (c3 * Q[k])) + (c4 * qc);           // mmc.py:535-538
+      const double x0v = sx[up_0(up[k])];
+      const double x1v = sx[up_1(up[k])];
+      // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
+      const bool raw = (t == 0 && carry);
+      auto qf = [&](double x) -> R {
+        const R xr = R(x);
+        return raw ? xr : rmax(xr, cs.qlb);
+      };
       const double dc1 = (double)c1;
       double acc = (double)b;                                         // utils.py:587-600 (fp64)
       acc = acc + (nup > 0 ? dc1 * x0v : 0.0);
@@ -228,23 +229,25 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteAr
       double hot = (double)qv;                                        // mmc.py:25-66 (hot start)
       hot = hot + (nup > 0 ? x0v : 0.0);
       hot = hot + (nup > 1 ? x1v : 0.0);
+      R inn = R(0);                                                   // I(t+1) = N @ Q_t, ascending columns
+      inn = inn + (nup > 0 ? qf(x0v) : R(0));
+      inn = inn + (nup > 1 ? qf(x1v) : R(0));
       if (nup > 2) {
         const int P = B.pos0 + r;
         const int bb = a.s.upb[P], c = a.s.upc[P];
         for (int j = 2; j < c; ++j) {
-          const double xj = sx[prv * S + a.s.uplist[bb + j]];
+          const double xj = sx[a.s.uplist[bb + j]];
           acc = acc + dc1 * xj;
           hot = hot + xj;
+          inn = inn + qf(xj);
         }
       }
+      const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
+      xk[k] = x;
       if (has[k] && t >= 0 && t < T) {
-        const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
         const R xr = R(x);
-        const R Qn = (t == 0 && carry) ? xr : rmax(xr, cs.qlb);        // mmc.py:557
-        sx[cur * S + r] = x;
-        sq[cur * S + r] = Q[k];
-        if (save) xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;
-        if (write_runoff) runoff[(int64_t)ref[k] * T + t] = (t == 0) ? rmax(xr, cs.qlb) : Qn;
+        const R Qn = raw ? xr : rmax(xr, cs.qlb);
+        xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;  // runoff is emitted from here (emit_runoff_kernel)
         if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
         if (t == T - 1) {
           if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
@@ -254,45 +257,65 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_forward_kernel(RouteAr
           }
         }
         Q[k] = Qn;
+        In[k] = inn;
       }
-      // one reach's chain in flight: interleaving more spills registers at KR = 8
+      // one reach's chain in flight keeps the register budget of 4 waves per SIMD
       __builtin_amdgcn_sched_barrier(0);
+    }
+    lds_barrier();
+    // ---- publish ------------------------------------------------------------------------------
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int t = tau - off[k];
+      if (has[k] && t >= 0 && t < T) sx[tid + k * BS] = xk[k];
+    }
+    if (vown) {
+      const int t = tau - v_off;
+      if (t >= 0 && t < T) sx[B.nloc + tid] = ring[tid * kChunk + (tau % kChunk)];
     }
     lds_barrier();
   };
 
   const int TT = (int)T + B.dmax;
   prefetch(0, qa);
-  for (int tau = 0; tau < TT; tau += 2) {
+  // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
+#pragma unroll 1
+  for (int tau = 0; tau < TT; ++tau) {
     tick(tau, qa, qb);
-    if (tau + 1 < TT) tick(tau + 1, qb, qa);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
 }
 
 // ============================================================================================
 // Backward (adjoint)
 // ============================================================================================
+// Reverse ticks; per tick:
+//   [import a chunk of (c1 gb, c2 gb) from downstream blocks]
+//   read:    the downstream reach's (c1_d gb_d, c2_d gb_d) from its slot (or the ring); export the
+//            consumers' values of virtual inflows to the upstream blocks            -- barrier --
+//   compute: VJP of one step, own slot <- (c1 gb, c2 gb)                             -- barrier --
 template <typename R, int KR>
-__global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteArgs a) {
+__global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sa = reinterpret_cast<double*>(smem);  // [2][S]  c1_i * gb_i  (fp64, transposed solve)
-  R* sb = reinterpret_cast<R*>(sa + 2 * S);       // [2][S]  c2_i * gb_i
-  double* ring = reinterpret_cast<double*>(smem + ((2 * S * (8 + sizeof(R)) + 15) / 16) * 16);
+  double* sa = reinterpret_cast<double*>(smem);  // [S] c1_i * gb_i  (fp64, transposed solve)
+  R* sb = reinterpret_cast<R*>(sa + S);           // [S] c2_i * gb_i
+  const StatTab<R> tab{sb + S, S};                // [6][S]
+  double* ring = reinterpret_cast<double*>(smem + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const R* xsave = static_cast<const R*>(a.x_save);
-  const R* gout = static_cast<const R*>(a.grad_out);
+  const R* gsch = static_cast<const R*>(a.gs);
   const R* qp = static_cast<const R*>(a.qprime);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
 
-  ReachStatic<R> st[KR];
   int ref[KR], off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
   unsigned up[KR];
   bool has[KR];
@@ -306,10 +329,10 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
     off[k] = a.s.off[P];
     dl[k] = a.s.dloc[P];
     up[k] = pack_up(a, P);
-    st[k] = load_static<R>(a, ref[k]);
     lam[k] = R(0);
     xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
+    if (has[k]) tab.put(r, load_static<R>(a, ref[k]));
   }
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
@@ -317,7 +340,6 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
     for (int k = 0; k < KR; ++k)
       if (has[k] && tid + k * BS == loc) dl[k] = -(c + 2);
   }
-  const bool gauge = a.g_roff != nullptr;
   const R* fs = static_cast<const R*>(a.fs);
   const bool vown = tid < B.nvirt;
   int v_edge = 0, v_off = 0, v_dloc = 0;
@@ -327,6 +349,7 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
     v_dloc = a.s.v_dloc[B.virt0 + tid];
   }
   const int TT = (int)T + B.dmax;
+  __syncthreads();
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
   auto load_own = [&](int tau, R(&dst)[KR]) {
@@ -347,17 +370,14 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
   // xp = x(t-1) of the step each reach runs at this tick; xn receives x(t-2) for the next tick
   auto tick = [&](int tb, R(&xp)[KR], R(&xn)[KR]) {
     const int tau = TT - 1 - tb;  // forward tick
-    const int cur = tb & 1, prv = cur ^ 1;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       ref[k] = opq(ref[k]);
       off[k] = opq(off[k]);
       up[k] = opq(up[k]);
       dl[k] = opq(dl[k]);
-      st[k] = opq_static(st[k]);
     }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
-      const int half = (tb / kChunk) & 1;
       for (int w = tid; w < B.ncout * kChunk; w += BS) {
         const int c = w / kChunk, sidx = w % kChunk;
         const int P = B.pos0 + a.s.cout_loc[B.cout0 + c];
@@ -368,19 +388,36 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
           A = wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2, a.status);
           Bv = wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2 + 1, a.status);
         }
-        ring[c * a.ring_stride + (half * kChunk + sidx) * 2] = A;
-        ring[c * a.ring_stride + (half * kChunk + sidx) * 2 + 1] = Bv;
+        ring[(c * kChunk + sidx) * 2] = A;
+        ring[(c * kChunk + sidx) * 2 + 1] = Bv;
       }
       lds_barrier();
     }
+    // ---- read ---------------------------------------------------------------------------------
     if (vown) {
       // export the consumer's (c1 gb, c2 gb) of step t to the upstream block
       const int t = tau - v_off;
       if (t >= 1 && t < T) {
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, sa[prv * S + v_dloc]);
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[prv * S + v_dloc]);
+        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, sa[v_dloc]);
+        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[v_dloc]);
       }
     }
+    double A[KR];
+    R Bd[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      A[k] = 0.0;
+      Bd[k] = R(0);
+      if (dl[k] >= 0) {
+        A[k] = sa[dl[k]];
+        Bd[k] = sb[dl[k]];
+      } else if (dl[k] <= -2) {
+        const int sidx = tb % kChunk;
+        A[k] = ring[((-dl[k] - 2) * kChunk + sidx) * 2];
+        Bd[k] = R(ring[((-dl[k] - 2) * kChunk + sidx) * 2 + 1]);
+      }
+    }
+    lds_barrier();
     load_own(tau - 2, xn);  // for the next tick
     // ---- compute (one reach at a time; its loads are issued first and consumed after the
     //      geometry recompute, which hides their latency) ------------------------------------
@@ -390,50 +427,31 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
       const int t = tau - off[k];
       const bool active = has[k] && t >= 1 && t < T;
       const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      R g[1], qv[1], xu[1][2], xup[1][2];
       const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + (r & (has[k] ? ~0 : 0))];  // own x(t)
-      {
-        g[0] = gauge ? R(0) : gout[(int64_t)ref[k] * T + tcl];
-        const int64_t row = tcl >= 1 ? tcl - 1 : 0;
-        qv[0] = qp[row * N + ref[k]];
-        xu[0][0] = up_x(up_0(up[k]), tau - 1, tcl);
-        xu[0][1] = up_x(up_1(up[k]), tau - 1, tcl);
-        xup[0][0] = up_x(up_0(up[k]), tau - 2, tcl - 1);
-        xup[0][1] = up_x(up_1(up[k]), tau - 2, tcl - 1);
-      }
-      // downstream adjoint (c1_d gb_d, c2_d gb_d): LDS slot of the previous tick, or imported
-      double A = 0.0;
-      R Bd = R(0);
-      if (dl[k] >= 0) {
-        A = sa[prv * S + dl[k]];
-        Bd = sb[prv * S + dl[k]];
-      } else if (dl[k] <= -2) {
-        const int sidx = (tb % (2 * kChunk));
-        A = ring[(-dl[k] - 2) * a.ring_stride + sidx * 2];
-        Bd = R(ring[(-dl[k] - 2) * a.ring_stride + sidx * 2 + 1]);
-      }
-      R gk = g[0];
-      if (gauge) {
-        const int64_t m0 = a.g_roff[ref[k]], m1 = a.g_roff[ref[k] + 1];
-        for (int64_t m = m0; m < m1; ++m) gk = gk + gout[a.g_rg[m] * T + tcl];
-      }
-      R qvk = qv[0];
+      const R gk = gsch[xs_base + (int64_t)tau * B.nloc + (r & (has[k] ? ~0 : 0))];  // dL/dQ_t (expand_grad_kernel)
+      const R qv0 = qp[(tcl >= 1 ? tcl - 1 : 0) * N + ref[k]];
+      const R xu0 = up_x(up_0(up[k]), tau - 1, tcl);
+      const R xu1 = up_x(up_1(up[k]), tau - 1, tcl);
+      const R xup0 = up_x(up_0(up[k]), tau - 2, tcl - 1);
+      const R xup1 = up_x(up_1(up[k]), tau - 2, tcl - 1);
+      const ReachStatic<R> st = tab.get(has[k] ? r : 0);
+      R qvk = qv0;
       if (fs) qvk = qvk * fs[ref[k]];                    // mmc.py:303-304
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
-      const double gb64 = (double)gx + A;                // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
+      const double gb64 = (double)gx + A[k];             // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
       const R gb = R(gb64);
       const R Qp = (t == 1 && carry) ? xp[k] : rmax(xp[k], cs.qlb);
       R c1, c2, c3, c4, tw, ss;
       Geom<R> geo;
-      coefficients<R>(st[k], Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
+      coefficients<R>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
       const int nup = up_n(up[k]);
       R Sx = R(0), I = R(0);
       const bool c0 = (t == 1 && carry);
-      Sx = Sx + (nup > 0 ? xu[0][0] : R(0));
-      Sx = Sx + (nup > 1 ? xu[0][1] : R(0));
-      I = I + (nup > 0 ? (c0 ? xup[0][0] : rmax(xup[0][0], cs.qlb)) : R(0));
-      I = I + (nup > 1 ? (c0 ? xup[0][1] : rmax(xup[0][1], cs.qlb)) : R(0));
+      Sx = Sx + (nup > 0 ? xu0 : R(0));
+      Sx = Sx + (nup > 1 ? xu1 : R(0));
+      I = I + (nup > 0 ? (c0 ? xup0 : rmax(xup0, cs.qlb)) : R(0));
+      I = I + (nup > 1 ? (c0 ? xup1 : rmax(xup1, cs.qlb)) : R(0));
       if (nup > 2) {
         const int P = B.pos0 + r;
         const int b = a.s.upb[P], c = a.s.upc[P];
@@ -447,7 +465,7 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
       const R qc = rmax(qvk, cs.qlb);
       const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
       R gQ, gn, gq, gp;
-      coefficients_vjp<R>(st[k], Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+      coefficients_vjp<R>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
       if (active) {
         pn[k] = pn[k] + gn;
         pq[k] = pq[k] + gq;
@@ -462,9 +480,9 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
           atomicAdd(g3 + 2, (double)pp[k]);
           pn[k] = pq[k] = pp[k] = R(0);
         }
-        sa[cur * S + r] = (double)c1 * gb64;
-        sb[cur * S + r] = c2 * gb;
-        lam[k] = ((gb * c3) + gQ) + Bd;
+        sa[r] = (double)c1 * gb64;
+        sb[r] = c2 * gb;
+        lam[k] = ((gb * c3) + gQ) + Bd[k];
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -473,9 +491,11 @@ __global__ void __launch_bounds__(kBlockThreads, 2) route_backward_kernel(RouteA
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2
   load_own(TT - 2, xa);
-  for (int tb = 0; tb < TT; tb += 2) {
+#pragma unroll 1
+  for (int tb = 0; tb < TT; ++tb) {
     tick(tb, xa, xb);
-    if (tb + 1 < TT) tick(tb + 1, xb, xa);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) xa[k] = xb[k];
   }
 }
 
@@ -487,6 +507,75 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
   gn[i] = R(gacc[3 * i + 0]);
   gq[i] = R(gacc[3 * i + 1]);
   gp[i] = R(gacc[3 * i + 2]);
+}
+
+// ============================================================================================
+// Layout transposes between the API's (reach, step) arrays and the schedule layout of x_save
+// (per workgroup, tick-major: row tau = t + off(r) holds its nloc reaches contiguously).  One
+// 256-thread workgroup per kTileR x kTileT tile; both sides coalesced through an LDS tile.
+// ============================================================================================
+// runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
+template <typename R>
+__global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
+  __shared__ R tile[kTileT][kTileR + 1];
+  const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
+  const BlockDesc B = a.s.blocks[b];
+  const int nr = min(kTileR, B.nloc - r0);
+  const int64_t T = a.T;
+  const int64_t t0 = (int64_t)blockIdx.y * kTileT;
+  const int64_t xs_base = T * B.pos0 + B.pre_dn;
+  const R* xs = static_cast<const R*>(a.x_save);
+  R* out = static_cast<R*>(a.runoff);
+  const R qlb = R(a.c[1]);
+  {
+    const int i = threadIdx.x % kTileR;  // reach (fastest: coalesced along the tick row)
+    if (i < nr) {
+      const int off = a.s.off[B.pos0 + r0 + i];
+      for (int j = threadIdx.x / kTileR; j < kTileT; j += 256 / kTileR)
+        if (t0 + j < T) tile[j][i] = xs[xs_base + (t0 + j + off) * B.nloc + r0 + i];
+    }
+  }
+  __syncthreads();
+  const int j = threadIdx.x % kTileT;    // step (fastest: coalesced along the reach row)
+  for (int i = threadIdx.x / kTileT; i < nr; i += 256 / kTileT) {
+    if (t0 + j < T) out[(int64_t)a.s.ref[B.pos0 + r0 + i] * T + t0 + j] = rmax(tile[j][i], qlb);
+  }
+}
+
+// gs[tick(t, r)] = dL/drunoff[ref(r), t], or in gauge mode sum over the reach's gauges g of
+// dL/dout[g, t] (mmc.py:405-411: every gauge sums the clamped discharge of its reaches)
+template <typename R>
+__global__ void __launch_bounds__(256) expand_grad_kernel(RouteArgs a) {
+  __shared__ R tile[kTileT][kTileR + 1];
+  const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
+  const BlockDesc B = a.s.blocks[b];
+  const int nr = min(kTileR, B.nloc - r0);
+  const int64_t T = a.T;
+  const int64_t t0 = (int64_t)blockIdx.y * kTileT;
+  const int64_t xs_base = T * B.pos0 + B.pre_dn;
+  const R* go = static_cast<const R*>(a.grad_out);
+  R* gs = static_cast<R*>(a.gs);
+  {
+    const int j = threadIdx.x % kTileT;
+    for (int i = threadIdx.x / kTileT; i < nr; i += 256 / kTileT) {
+      if (t0 + j >= T) continue;
+      const int64_t ref = a.s.ref[B.pos0 + r0 + i];
+      R g = R(0);
+      if (a.g_roff) {
+        for (int64_t m = a.g_roff[ref]; m < a.g_roff[ref + 1]; ++m) g = g + go[a.g_rg[m] * T + t0 + j];
+      } else {
+        g = go[ref * T + t0 + j];
+      }
+      tile[j][i] = g;
+    }
+  }
+  __syncthreads();
+  const int i = threadIdx.x % kTileR;
+  if (i < nr) {
+    const int off = a.s.off[B.pos0 + r0 + i];
+    for (int j = threadIdx.x / kTileR; j < kTileT; j += 256 / kTileR)
+      if (t0 + j < T) gs[xs_base + (t0 + j + off) * B.nloc + r0 + i] = tile[j][i];
+  }
 }
 
 // ============================================================================================
@@ -516,18 +605,14 @@ __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
 // ============================================================================================
 template <typename R>
 size_t route_smem_bytes(const Graph* g, bool backward) {
-  const size_t S = (size_t)g->max_slots;
-  size_t base = ((2 * S * (8 + sizeof(R)) + 15) / 16) * 16;
-  const int nring = backward ? g->max_cout : g->max_virt;
-  const size_t ring = backward ? 2 * 2 * kChunk : 2 * kChunk;
-  return base + (size_t)nring * ring * sizeof(double);
+  return route_lds_bytes((size_t)g->max_slots, (size_t)(backward ? g->max_cout : g->max_virt), backward, sizeof(R));
 }
 
 template <typename R, int KR>
 hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream_t stream) {
   const size_t smem = route_smem_bytes<R>(g, backward);
   a.slot_stride = g->max_slots;
-  a.ring_stride = backward ? 4 * kChunk : 2 * kChunk;
+  a.ring_stride = backward ? 2 * kChunk : kChunk;
   a.n_cut = g->n_cut;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
@@ -554,8 +639,7 @@ hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipSt
   switch (g->kr) {
     case 1: return launch_route_kr<R, 1>(g, a, backward, stream);
     case 2: return launch_route_kr<R, 2>(g, a, backward, stream);
-    case 4: return launch_route_kr<R, 4>(g, a, backward, stream);
-    default: return launch_route_kr<R, 8>(g, a, backward, stream);
+    default: return launch_route_kr<R, 4>(g, a, backward, stream);
   }
 }
 
@@ -567,13 +651,28 @@ int max_resident_blocks(const Graph* g, bool backward) {
   switch (g->kr) {
     case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1>; break;
     case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2>; break;
-    case 4: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4>; break;
-    default: f = backward ? (const void*)route_backward_kernel<R, 8> : (const void*)route_forward_kernel<R, 8>;
+    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4>;
   }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) != hipSuccess) return -1;
   return nb * prop.multiProcessorCount;
+}
+
+template <typename R>
+hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream) {
+  if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
+  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + kTileT - 1) / kTileT));
+  hipLaunchKernelGGL(emit_runoff_kernel<R>, grid, dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream) {
+  if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
+  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + kTileT - 1) / kTileT));
+  hipLaunchKernelGGL(expand_grad_kernel<R>, grid, dim3(256), 0, stream, a);
+  return hipGetLastError();
 }
 
 template <typename R>
@@ -590,6 +689,10 @@ template hipError_t launch_route<float>(const Graph*, const RouteArgs&, bool, hi
 template hipError_t launch_route<double>(const Graph*, const RouteArgs&, bool, hipStream_t);
 template int max_resident_blocks<float>(const Graph*, bool);
 template int max_resident_blocks<double>(const Graph*, bool);
+template hipError_t launch_emit_runoff<float>(const Graph*, const RouteArgs&, hipStream_t);
+template hipError_t launch_emit_runoff<double>(const Graph*, const RouteArgs&, hipStream_t);
+template hipError_t launch_expand_grad<float>(const Graph*, const RouteArgs&, hipStream_t);
+template hipError_t launch_expand_grad<double>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_gauge<float>(const GaugeArgs&, const float*, float*, hipStream_t);
 template hipError_t launch_gauge<double>(const GaugeArgs&, const double*, double*, hipStream_t);
 

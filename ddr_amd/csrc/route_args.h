@@ -31,6 +31,7 @@ struct RouteArgs {
   void* ss_last;
   // backward
   const void* grad_out;
+  void* gs;              // grad_out expanded to the schedule layout of x_save (backward workspace)
   const int64_t* g_roff;
   const int64_t* g_rg;
   double* bwd_bnd;
@@ -56,6 +57,10 @@ template <typename R>
 hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipStream_t stream);
 template <typename R>
 int max_resident_blocks(const Graph* g, bool backward);
+template <typename R>
+hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream);
+template <typename R>
+hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream);
 template <typename R>
 hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t stream);
 

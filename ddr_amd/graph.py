@@ -161,8 +161,10 @@ class RiverGraph:
     def bnd_numel(self, T: int) -> int:
         return self.info.bnd_elems_per_t * T
 
-    def bwd_numel(self, T: int) -> int:
-        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed
+    def bwd_numel(self, T: int, itemsize: int = 4) -> int:
+        """Backward workspace in doubles: boundary + accumulators, then the gradient expanded to
+        the x_save layout in reals of ``itemsize`` bytes."""
+        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed + -(-self.save_numel(T) * itemsize // 8)
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:

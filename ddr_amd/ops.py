@@ -107,7 +107,7 @@ def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Te
     save = bool(flags & _lib.DDR_FWD_SAVE_X) or gauge
     fflags = flags | (_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_NO_RUNOFF if gauge else 0)
     runoff = torch.empty((G, T), device=dev, dtype=dt)
-    x_save = torch.empty(g.save_numel(T) if save else 0, device=dev, dtype=dt)
+    x_save = torch.empty(g.save_numel(T), device=dev, dtype=dt)  # always written (runoff is staged here)
     bnd = torch.empty(g.bnd_numel(T), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
     q_last = torch.empty(N, device=dev, dtype=dt)
@@ -119,7 +119,7 @@ def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Te
     r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
     c = _consts(consts)
     _lib.check(fwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, _lib.ptr(q0), runoff.data_ptr(),
-                   x_save.data_ptr() if save else None, bnd.data_ptr() if bnd.numel() else None, status.data_ptr(),
+                   x_save.data_ptr(), bnd.data_ptr() if bnd.numel() else None, status.data_ptr(),
                    q_last.data_ptr(), tw.data_ptr(), ss.data_ptr(), int(fflags), stream))
     if gauge:
         red = lib.ddr_gauge_reduce_f32 if dt == torch.float32 else lib.ddr_gauge_reduce_f64
@@ -136,9 +136,8 @@ def _(qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r
     T, N = qprime.shape
     G = g_off.shape[0] - 1 if g_off is not None else N
     g = _graph(graph_id)
-    save = bool(flags & _lib.DDR_FWD_SAVE_X) or g_off is not None
     return (qprime.new_empty((G, T)), qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N),
-            qprime.new_empty(g.save_numel(T) if save else 0), qprime.new_empty(g.bnd_numel(T), dtype=torch.float64))
+            qprime.new_empty(g.save_numel(T)), qprime.new_empty(g.bnd_numel(T), dtype=torch.float64))
 
 
 @torch.library.custom_op("ddrx::mc_route_backward", mutates_args=())
@@ -155,7 +154,7 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
     gn = torch.empty(N, device=dev, dtype=dt)
     gq = torch.empty(N, device=dev, dtype=dt)
     gp = torch.empty(N, device=dev, dtype=dt)
-    bwd_bnd = torch.empty(g.bwd_numel(T), device=dev, dtype=torch.float64)
+    bwd_bnd = torch.empty(g.bwd_numel(T, qprime.element_size()), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
     lib = _lib.load()
     bwd = lib.ddr_mc_backward_f32 if dt == torch.float32 else lib.ddr_mc_backward_f64

@@ -71,8 +71,8 @@ typedef struct {
   int64_t save_elems_per_t;   /* x_save elements = save_elems_per_t * T + save_elems_fixed  */
   int64_t save_elems_fixed;
   int64_t bnd_elems_per_t;    /* forward boundary buffer doubles = bnd_elems_per_t * T     */
-  int64_t bwd_elems_per_t;    /* backward workspace doubles = bwd_elems_per_t * T          */
-  int64_t bwd_elems_fixed;    /*                            + bwd_elems_fixed              */
+  int64_t bwd_elems_per_t;    /* backward workspace = 8 * (bwd_elems_per_t * T + bwd_elems_fixed) */
+  int64_t bwd_elems_fixed;    /*   bytes + sizeof(real) * (x_save elements), 8-byte aligned      */
   int64_t status_bytes;       /* device status word block (zeroed by the library)          */
 } ddr_graph_info;
 
@@ -128,13 +128,15 @@ typedef struct {
   const int64_t* reach_gauges;   /* (offsets[G]) gauge id of each membership      */
 } ddr_gauges;
 
+/* DDR_FWD_SAVE_X is accepted for compatibility: x_save is always written. */
 enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4 };
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
  *   qprime     (T, N) lateral inflow, time-major, reference order
  *   q0         (N) carried discharge (DDR_FWD_CARRY) or NULL
- *   runoff     (N, T) (or (G, T) via ddr_gauge_reduce afterwards; pass DDR_FWD_NO_RUNOFF)
- *   x_save     internal layout, see ddr_graph_info (DDR_FWD_SAVE_X), else may be NULL
+ *   runoff     (N, T), or NULL / DDR_FWD_NO_RUNOFF (e.g. gauges: ddr_gauge_reduce afterwards)
+ *   x_save     required: the routed states in the schedule layout (save_elems_per_t * T +
+ *              save_elems_fixed reals); runoff is emitted from it by a tiled transpose
  *   bnd        forward boundary buffer (bnd_elems_per_t * T doubles; may be NULL if n_cut == 0);
  *              must be kept unchanged for ddr_mc_backward
  *   status     device status block (status_bytes)
@@ -151,6 +153,7 @@ ddr_status ddr_mc_forward_f64(const ddr_graph* g, const ddr_mc_consts* c, const 
                               void* stream);
 
 /* Reverse-time, reverse-topological adjoint.  grad_runoff is (N, T), or (G, T) with gauges != NULL.
+ * bwd_bnd is the backward workspace (size in ddr_graph_info).
  * Writes per-reach dL/dn, dL/dq_spatial, dL/dp_spatial (N each; for a scalar p the caller sums). */
 ddr_status ddr_mc_backward_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
                                const float* qprime, int64_t T, const float* x_save,
@@ -163,7 +166,7 @@ ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const
                                double* bwd_bnd, void* status, double* grad_n, double* grad_q,
                                double* grad_p, int32_t flags, void* stream);
 
-/* Gauge reduction of a forward's saved states (requires DDR_FWD_SAVE_X): runoff (G, T). */
+/* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,
                                 float* runoff, void* stream);

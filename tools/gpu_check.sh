@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU-side check: parity tests, then one bench line (no CPU baseline) under a kernel trace.
+# Usage: bash tools/gpu_check.sh [tag]
+TAG=${1:-check}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export DDR_CHECK_STATUS=1
+timeout -k 10 600 python -m pytest $R/tests -q -m gpu -x > $OUT/pytest.log 2>&1
+rc=$?
+grep -E "passed|failed|FAILED|^E  " $OUT/pytest.log | cut -c1-300 | head -20
+[ $rc -ne 0 ] && { echo "PYTEST FAILED rc=$rc"; exit $rc; }
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench.log 2>&1
+rc=$?
+grep '^{' $OUT/bench.log | cut -c1-600
+find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+[ -f $OUT/kernel_stats.csv ] && cut -d, -f1-8 $OUT/kernel_stats.csv | cut -c1-200 | head -8
+exit $rc
