@@ -33,9 +33,11 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16;
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
 //   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64
 //   backward: A slots (f64) | B slots (R) | 6 statics (R) | ring [ncout][kChunk][2] f64
+// (after the math tables of fastmath.h, which occupy the first kMathTabBytes)
+constexpr size_t kMathTabBytes = 3072;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nring, bool backward, size_t rsize) {
   const size_t base = backward ? slots * (8 + rsize + 6 * rsize) : slots * (8 + 6 * rsize);
-  return align16(base) + nring * kChunk * (backward ? 16 : 8);
+  return kMathTabBytes + align16(base) + nring * kChunk * (backward ? 16 : 8);
 }
 
 // One workgroup's slice of the schedule.  Reaches of a block occupy internal positions

@@ -28,6 +28,7 @@ namespace ddr {
 namespace {
 
 constexpr unsigned long long kSentinel = ~0ull;
+static_assert(kMathTabBytes == (2 * kLnTabN + kExpTabN) * sizeof(double), "math table size");
 
 
 __device__ __forceinline__ void lds_barrier() {
@@ -133,9 +134,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int tid = threadIdx.x;
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sx = reinterpret_cast<double*>(smem);                         // [S] x_j(t), solve precision
+  double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
   const StatTab<R> tab{reinterpret_cast<R*>(sx + S), S};                // [6][S]
-  double* ring = reinterpret_cast<double*>(smem + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
+  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const int64_t N = a.N;
@@ -166,6 +167,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const bool vown = tid < B.nvirt;
   int v_off = 0;
   if (vown) v_off = a.s.v_off[B.virt0 + tid];
+  load_math_tables();
   __syncthreads();
 
   // q'[max(t-1,0)] (or the carried Q0 at t = 0) for the step each reach runs at tick `tau`
@@ -302,10 +304,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int tid = threadIdx.x;
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sa = reinterpret_cast<double*>(smem);  // [S] c1_i * gb_i  (fp64, transposed solve)
-  R* sb = reinterpret_cast<R*>(sa + S);           // [S] c2_i * gb_i
-  const StatTab<R> tab{sb + S, S};                // [6][S]
-  double* ring = reinterpret_cast<double*>(smem + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
+  double* sa = reinterpret_cast<double*>(smem + kMathTabBytes);  // [S] c1_i * gb_i  (fp64, transposed solve)
+  R* sb = reinterpret_cast<R*>(sa + S);                           // [S] c2_i * gb_i
+  const StatTab<R> tab{sb + S, S};                                // [6][S]
+  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const int64_t N = a.N;
@@ -349,6 +351,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     v_dloc = a.s.v_dloc[B.virt0 + tid];
   }
   const int TT = (int)T + B.dmax;
+  load_math_tables();
   __syncthreads();
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)

@@ -14,6 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench.log 2>&1
 rc=$?
 grep '^{' $OUT/bench.log | cut -c1-600
-find $OUT/prof -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
-[ -f $OUT/kernel_stats.csv ] && cut -d, -f1-8 $OUT/kernel_stats.csv | cut -c1-200 | head -8
+python3 $R/tools/kstats.py $(find $OUT/prof -name "*.db") > $OUT/kernel_stats.txt 2>&1
+head -8 $OUT/kernel_stats.txt
+find $OUT/prof -name "*.db" -delete
 exit $rc
