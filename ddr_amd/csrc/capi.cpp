@@ -68,6 +68,7 @@ void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr
   a.c[5] = c->bottom_width_lb;
   a.c[6] = c->side_slope_lb;
   a.c[7] = c->side_slope_ub;
+  for (int i = 0; i < 8; ++i) a.cf[i] = (float)a.c[i];
 }
 
 template <typename R>

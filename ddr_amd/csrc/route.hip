@@ -61,9 +61,16 @@ __device__ double wait_granule(const double* p, unsigned* status) {
   return __longlong_as_double(v);
 }
 
+// Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
 template <typename R>
-__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a) {
-  return Consts<R>{R(a.c[0]), R(a.c[1]), R(a.c[2]), R(a.c[3]), R(a.c[4]), R(a.c[5]), R(a.c[6]), R(a.c[7])};
+__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a);
+template <>
+__device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a) {
+  return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7]};
+}
+template <>
+__device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a) {
+  return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7]};
 }
 
 template <typename R>
@@ -148,13 +155,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   int ref[KR], off[KR];
   unsigned up[KR];
-  bool has[KR], cut[KR];
+  bool cut[KR];
   R Q[KR], In[KR], fsr[KR], qa[KR], qb[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
-    has[k] = r < B.nloc;
-    const int P = B.pos0 + (has[k] ? r : 0);
+    const bool hk = r < B.nloc;
+    const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
     up[k] = pack_up(a, P);
@@ -162,7 +169,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     fsr[k] = a.fs ? static_cast<const R*>(a.fs)[ref[k]] : R(1);  // mmc.py:303-304 (q' * flow_scale)
     Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
-    if (has[k]) tab.put(r, load_static<R>(a, ref[k]));
+    if (hk) tab.put(r, load_static<R>(a, ref[k]));
   }
   const bool vown = tid < B.nvirt;
   int v_off = 0;
@@ -183,6 +190,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR]) {
+    // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
+    // instead of being hoisted into registers held across the loop
+    const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       ref[k] = opq(ref[k]);
@@ -207,10 +217,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // ---- compute: one reach at a time (gather, physics, fp64 column sweep) -------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const int r = tid + k * BS;
+      const int r = tq + k * BS;
+      const bool hk = r < B.nloc;
       const int t = tau - off[k];
       const int nup = up_n(up[k]);
-      const ReachStatic<R> st = tab.get(has[k] ? r : 0);
+      const ReachStatic<R> st = tab.get(hk ? r : 0);
       const R qv = qcur[k] * fsr[k];
       R c1, c2, c3, c4, tw, ss;
       coefficients<R>(st, Q[k], cs, c1, c2, c3, c4, tw, ss);
@@ -246,7 +257,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
       xk[k] = x;
-      if (has[k] && t >= 0 && t < T) {
+      if (hk && t >= 0 && t < T) {
         const R xr = R(x);
         const R Qn = raw ? xr : rmax(xr, cs.qlb);
         xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;  // runoff is emitted from here (emit_runoff_kernel)
@@ -269,7 +280,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int t = tau - off[k];
-      if (has[k] && t >= 0 && t < T) sx[tid + k * BS] = xk[k];
+      const int r = tq + k * BS;
+      if (r < B.nloc && t >= 0 && t < T) sx[r] = xk[k];
     }
     if (vown) {
       const int t = tau - v_off;
@@ -320,13 +332,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   int ref[KR], off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
   unsigned up[KR];
-  bool has[KR];
   R lam[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
-    has[k] = r < B.nloc;
-    const int P = B.pos0 + (has[k] ? r : 0);
+    const bool hk = r < B.nloc;
+    const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
     dl[k] = a.s.dloc[P];
@@ -334,13 +345,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     lam[k] = R(0);
     xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
-    if (has[k]) tab.put(r, load_static<R>(a, ref[k]));
+    if (hk) tab.put(r, load_static<R>(a, ref[k]));
   }
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
 #pragma unroll
     for (int k = 0; k < KR; ++k)
-      if (has[k] && tid + k * BS == loc) dl[k] = -(c + 2);
+      if (tid + k * BS == loc) dl[k] = -(c + 2);
   }
   const R* fs = static_cast<const R*>(a.fs);
   const bool vown = tid < B.nvirt;
@@ -355,10 +366,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   __syncthreads();
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
-  auto load_own = [&](int tau, R(&dst)[KR]) {
+  auto load_own = [&](int tau, R(&dst)[KR], int tq) {
     const int tc = tau < 0 ? 0 : (tau >= TT ? TT - 1 : tau);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + ((tid + k * BS) & (has[k] ? ~0 : 0))];
+    for (int k = 0; k < KR; ++k) {
+      const int r = tq + k * BS;
+      dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + (r < B.nloc ? r : 0)];
+    }
   };
   auto up_x = [&](int u, int tick, int64_t t) -> R {
     if (u < B.nloc) {
@@ -373,6 +387,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // xp = x(t-1) of the step each reach runs at this tick; xn receives x(t-2) for the next tick
   auto tick = [&](int tb, R(&xp)[KR], R(&xn)[KR]) {
     const int tau = TT - 1 - tb;  // forward tick
+    const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       ref[k] = opq(ref[k]);
@@ -421,23 +436,25 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     }
     lds_barrier();
-    load_own(tau - 2, xn);  // for the next tick
+    load_own(tau - 2, xn, tq);  // for the next tick
     // ---- compute (one reach at a time; its loads are issued first and consumed after the
     //      geometry recompute, which hides their latency) ------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const int r = tid + k * BS;
+      const int r = tq + k * BS;
+      const bool hk = r < B.nloc;
+      const int rs = hk ? r : 0;
       const int t = tau - off[k];
-      const bool active = has[k] && t >= 1 && t < T;
+      const bool active = hk && t >= 1 && t < T;
       const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + (r & (has[k] ? ~0 : 0))];  // own x(t)
-      const R gk = gsch[xs_base + (int64_t)tau * B.nloc + (r & (has[k] ? ~0 : 0))];  // dL/dQ_t (expand_grad_kernel)
+      const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + rs];  // own x(t)
+      const R gk = gsch[xs_base + (int64_t)tau * B.nloc + rs];    // dL/dQ_t (expand_grad_kernel)
       const R qv0 = qp[(tcl >= 1 ? tcl - 1 : 0) * N + ref[k]];
       const R xu0 = up_x(up_0(up[k]), tau - 1, tcl);
       const R xu1 = up_x(up_1(up[k]), tau - 1, tcl);
       const R xup0 = up_x(up_0(up[k]), tau - 2, tcl - 1);
       const R xup1 = up_x(up_1(up[k]), tau - 2, tcl - 1);
-      const ReachStatic<R> st = tab.get(has[k] ? r : 0);
+      const ReachStatic<R> st = tab.get(rs);
       R qvk = qv0;
       if (fs) qvk = qvk * fs[ref[k]];                    // mmc.py:303-304
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
@@ -493,7 +510,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2
-  load_own(TT - 2, xa);
+  load_own(TT - 2, xa, tid);
 #pragma unroll 1
   for (int tb = 0; tb < TT; ++tb) {
     tick(tb, xa, xb);

@@ -39,6 +39,7 @@ struct RouteArgs {
   void* gq;
   void* gp;
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
+  float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
 };
 
 struct GaugeArgs {
