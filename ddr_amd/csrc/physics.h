@@ -33,6 +33,37 @@ __device__ __forceinline__ double pw(double x, double y, double* ln_x = nullptr)
 __device__ __forceinline__ float rsqrt_(float a) { return sqrtf(a); }
 __device__ __forceinline__ double rsqrt_(double a) { return sqrt(a); }
 
+// Operation set of the physics: Fast = false is the bit-exact set above (forward); Fast = true is
+// used by the fp32 adjoint's recompute and VJP, whose tolerance (gradients, 1e-4) allows hardware
+// approximations: v_rcp_f32 division (~1.5 ulp), v_log_f32 / v_exp_f32 pow (~1e-6 relative),
+// v_sqrt_f32.  The fp64 build always uses the exact set.
+template <bool Fast>
+__device__ __forceinline__ float dvf(float a, float b) {
+  if constexpr (Fast) return a * __builtin_amdgcn_rcpf(b);
+  else return div_rn(a, b);
+}
+template <bool Fast>
+__device__ __forceinline__ double dvf(double a, double b) { return a / b; }
+template <bool Fast>
+__device__ __forceinline__ float pwf(float x, float y, double* ln_x = nullptr) {
+  if constexpr (Fast) {
+    const float l2 = __builtin_amdgcn_logf(x);  // log2 x
+    if (ln_x) *ln_x = (double)(l2 * 0.69314718f);
+    return __builtin_amdgcn_exp2f(y * l2);
+  } else {
+    return pow_pos(x, y, ln_x);
+  }
+}
+template <bool Fast>
+__device__ __forceinline__ double pwf(double x, double y, double* ln_x = nullptr) { return pw(x, y, ln_x); }
+template <bool Fast>
+__device__ __forceinline__ float sqf(float a) {
+  if constexpr (Fast) return __builtin_amdgcn_sqrtf(a);
+  else return sqrtf(a);
+}
+template <bool Fast>
+__device__ __forceinline__ double sqf(double a) { return sqrt(a); }
+
 template <typename R>
 __device__ __forceinline__ R rmax(R a, R b) { return a > b ? a : b; }  // torch.clamp(min=) on finite
 template <typename R>
@@ -63,7 +94,7 @@ struct ReachStatic {
 // The six stored fields (n, qe, p, sqrtS, L, X) -> the derived ones.  The routing kernels keep only
 // the stored fields (in LDS) and call this every tick; the operations are the same as at
 // construction, so the values are identical.
-template <typename R>
+template <typename R, bool Fast = false>
 __device__ __forceinline__ ReachStatic<R> derive_static(R n, R qe, R p, R sqrtS, R L, R X) {
   ReachStatic<R> s;
   s.n = n;
@@ -71,8 +102,8 @@ __device__ __forceinline__ ReachStatic<R> derive_static(R n, R qe, R p, R sqrtS,
   s.p = p;
   s.sqrtS = sqrtS;
   s.dd = (p * sqrtS) + R(1e-8);
-  s.expo = dv(R(3), R(5) + R(3) * qe);
-  s.inv_n = dv(R(1), n);
+  s.expo = dvf<Fast>(R(3), R(5) + R(3) * qe);
+  s.inv_n = dvf<Fast>(R(1), n);
   s.L = L;
   s.X = X;
   return s;
@@ -89,37 +120,37 @@ struct Geom {
   R ratio, pw, depth, dq, tw, ssr, ss, bwr, bw, area, sq, wp, Rh, r23, v, cel, twok, den, ln_ratio, ln_depth;
 };
 
-template <typename R>
+template <typename R, bool Fast = false>
 __device__ __forceinline__ void coefficients(const ReachStatic<R>& s, R Q, const Consts<R>& c,
                                              R& c1, R& c2, R& c3, R& c4, R& tw_out, R& ss_out,
                                              Geom<R>* gk = nullptr) {
   double ln_ratio = 0.0, ln_depth = 0.0;
   const R num = (Q * s.n) * s.qe1();
-  const R ratio = dv(num, s.dd);
-  const R pwv = pw(ratio, s.expo, gk ? &ln_ratio : nullptr);
+  const R ratio = dvf<Fast>(num, s.dd);
+  const R pwv = pwf<Fast>(ratio, s.expo, gk ? &ln_ratio : nullptr);
   const R depth = rmax(pwv, c.dlb);
-  const R dq = pw(depth, s.qe, gk ? &ln_depth : nullptr);
+  const R dq = pwf<Fast>(depth, s.qe, gk ? &ln_depth : nullptr);
   const R tw = s.p * dq;
-  const R ssr = dv(tw * s.qe, R(2) * depth);
+  const R ssr = dvf<Fast>(tw * s.qe, R(2) * depth);
   const R ss = rmin(rmax(ssr, c.sslb), c.ssub);
   const R bwr = tw - (R(2) * ss) * depth;
   const R bw = rmax(bwr, c.bwlb);
   const R area = ((tw + bw) * depth) * R(0.5);  // x / 2 == x * 0.5 exactly
-  const R sq = rsqrt_(R(1) + ss * ss);
+  const R sq = sqf<Fast>(R(1) + ss * ss);
   const R wp = bw + (R(2) * depth) * sq;
-  const R Rh = dv(area, wp);
-  const R r23 = pw(Rh, two_thirds<R>());
+  const R Rh = dvf<Fast>(area, wp);
+  const R r23 = pwf<Fast>(Rh, two_thirds<R>());
   const R v = (s.inv_n * r23) * s.sqrtS;
   const R vc = rmin(rmax(v, c.vlb), c.vub);
-  const R cel = dv(vc * R(5), R(3));
-  const R k = dv(s.L, cel);
+  const R cel = dvf<Fast>(vc * R(5), R(3));
+  const R k = dvf<Fast>(s.L, cel);
   const R twok = R(2) * k;
   const R omX = s.omX();
   const R den = (twok * omX) + c.dt;
-  c1 = dv(c.dt - twok * s.X, den);
-  c2 = dv(c.dt + twok * s.X, den);
-  c3 = dv((twok * omX) - c.dt, den);
-  c4 = dv(R(2) * c.dt, den);
+  c1 = dvf<Fast>(c.dt - twok * s.X, den);
+  c2 = dvf<Fast>(c.dt + twok * s.X, den);
+  c3 = dvf<Fast>((twok * omX) - c.dt, den);
+  c4 = dvf<Fast>(R(2) * c.dt, den);
   tw_out = tw;
   ss_out = ss;
   if (gk) {
@@ -131,30 +162,30 @@ __device__ __forceinline__ void coefficients(const ReachStatic<R>& s, R Q, const
 }
 
 // VJP of (c1, c2, c3, c4) w.r.t. (Q, n, q_spatial, p_spatial) at the point described by g.
-template <typename R>
+template <typename R, bool Fast = false>
 __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, const Consts<R>& c,
                                                  const Geom<R>& g, R c1, R c2, R c3, R c4, R gc1,
                                                  R gc2, R gc3, R gc4, R& gQ, R& gn, R& gq, R& gp) {
   // c_k(twok): d c1 = (-X - c1 (1-X)) / den, d c2 = (X - c2 (1-X)) / den,
   //            d c3 = (1-X)(1 - c3) / den,   d c4 = -c4 (1-X) / den
   const R omX = s.omX();
-  const R g_twok = dv(gc1 * (-s.X - c1 * omX) + gc2 * (s.X - c2 * omX) + gc3 * omX * (R(1) - c3) -
+  const R g_twok = dvf<Fast>(gc1 * (-s.X - c1 * omX) + gc2 * (s.X - c2 * omX) + gc3 * omX * (R(1) - c3) -
                           gc4 * c4 * omX, g.den);
   const R k = g.twok * R(0.5);
   const R g_k = R(2) * g_twok;
-  const R g_cel = dv(-g_k * k, g.cel);
+  const R g_cel = dvf<Fast>(-g_k * k, g.cel);
   const bool vin = (g.v >= c.vlb) && (g.v <= c.vub);
-  const R g_v = vin ? g_cel * dv(R(5), R(3)) : R(0);
+  const R g_v = vin ? g_cel * dvf<Fast>(R(5), R(3)) : R(0);
   // v = inv_n * R^(2/3) * sqrtS
-  const R g_Rh = dv(g_v * s.inv_n * s.sqrtS * two_thirds<R>() * g.r23, g.Rh);
+  const R g_Rh = dvf<Fast>(g_v * s.inv_n * s.sqrtS * two_thirds<R>() * g.r23, g.Rh);
   R g_n = -g_v * g.v * s.inv_n;
   // Rh = area / wp
-  const R g_area = dv(g_Rh, g.wp);
-  const R g_wp = dv(-g_Rh * g.Rh, g.wp);
+  const R g_area = dvf<Fast>(g_Rh, g.wp);
+  const R g_wp = dvf<Fast>(-g_Rh * g.Rh, g.wp);
   // wp = bw + 2 depth sq
   R g_bw = g_wp;
   R g_depth = g_wp * R(2) * g.sq;
-  R g_ss = dv(g_wp * R(2) * g.depth * g.ss, g.sq);
+  R g_ss = dvf<Fast>(g_wp * R(2) * g.depth * g.ss, g.sq);
   // area = (tw + bw) depth / 2
   R g_tw = g_area * g.depth * R(0.5);
   g_bw += g_area * g.depth * R(0.5);
@@ -166,7 +197,7 @@ __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, c
   g_depth -= R(2) * g.ss * g_bwr;
   // ss = clamp(tw qe / (2 depth))
   const R g_ssr = (g.ssr >= c.sslb && g.ssr <= c.ssub) ? g_ss : R(0);
-  const R inv2d = dv(R(1), R(2) * g.depth);
+  const R inv2d = dvf<Fast>(R(1), R(2) * g.depth);
   g_tw += g_ssr * s.qe * inv2d;
   R g_qe = g_ssr * g.tw * inv2d;
   g_depth -= g_ssr * g.ssr * R(2) * inv2d;
@@ -177,12 +208,12 @@ __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, c
   // depth = max(pw, d_lb)
   const R g_pw = (g.pw >= c.dlb) ? g_depth : R(0);
   // pw = ratio^e ; e = 3 / (5 + 3 qe), de/dqe = -9 / (5 + 3qe)^2 = -e^2
-  const R g_ratio = dv(g_pw * s.expo * g.pw, g.ratio);
+  const R g_ratio = dvf<Fast>(g_pw * s.expo * g.pw, g.ratio);
   const R g_e = g_pw * g.pw * g.ln_ratio;
   g_qe -= g_e * s.expo * s.expo;
   // ratio = num / (p sqrtS + 1e-8)
-  const R g_num = dv(g_ratio, s.dd);
-  g_p -= dv(g_ratio * g.ratio, s.dd) * s.sqrtS;
+  const R g_num = dvf<Fast>(g_ratio, s.dd);
+  g_p -= dvf<Fast>(g_ratio * g.ratio, s.dd) * s.sqrtS;
   // num = Q n (qe + 1)
   const R qe1 = s.qe1();
   gQ = g_num * s.n * qe1;

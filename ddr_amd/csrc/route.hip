@@ -120,8 +120,9 @@ struct StatTab {
     s[4 * S + r] = v.L;
     s[5 * S + r] = v.X;
   }
+  template <bool Fast = false>
   __device__ __forceinline__ ReachStatic<R> get(int r) const {
-    return derive_static<R>(s[r], s[S + r], s[2 * S + r], s[3 * S + r], s[4 * S + r], s[5 * S + r]);
+    return derive_static<R, Fast>(s[r], s[S + r], s[2 * S + r], s[3 * S + r], s[4 * S + r], s[5 * S + r]);
   }
 };
 
@@ -454,7 +455,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const R xu1 = up_x(up_1(up[k]), tau - 1, tcl);
       const R xup0 = up_x(up_0(up[k]), tau - 2, tcl - 1);
       const R xup1 = up_x(up_1(up[k]), tau - 2, tcl - 1);
-      const ReachStatic<R> st = tab.get(rs);
+      const ReachStatic<R> st = tab.template get<true>(rs);
       R qvk = qv0;
       if (fs) qvk = qvk * fs[ref[k]];                    // mmc.py:303-304
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
@@ -464,7 +465,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const R Qp = (t == 1 && carry) ? xp[k] : rmax(xp[k], cs.qlb);
       R c1, c2, c3, c4, tw, ss;
       Geom<R> geo;
-      coefficients<R>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
+      coefficients<R, true>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
       const int nup = up_n(up[k]);
       R Sx = R(0), I = R(0);
       const bool c0 = (t == 1 && carry);
@@ -485,7 +486,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const R qc = rmax(qvk, cs.qlb);
       const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
       R gQ, gn, gq, gp;
-      coefficients_vjp<R>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+      coefficients_vjp<R, true>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
       if (active) {
         pn[k] = pn[k] + gn;
         pq[k] = pq[k] + gq;
@@ -534,31 +535,48 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
 // (per workgroup, tick-major: row tau = t + off(r) holds its nloc reaches contiguously).  One
 // 256-thread workgroup per kTileR x kTileT tile; both sides coalesced through an LDS tile.
 // ============================================================================================
+// Each thread moves kTileT * kTileR / 256 = 16 elements: all 16 loads are issued before the first
+// is consumed (memory-level parallelism), and the tile's reference ids are staged in LDS so the
+// scattered side has no dependent global loads.
+constexpr int kTrPer = kTileR * kTileT / 256;
+
 // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
 template <typename R>
 __global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
   __shared__ R tile[kTileT][kTileR + 1];
+  __shared__ int sref[kTileR];
   const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
   const BlockDesc B = a.s.blocks[b];
   const int nr = min(kTileR, B.nloc - r0);
   const int64_t T = a.T;
   const int64_t t0 = (int64_t)blockIdx.y * kTileT;
-  const int64_t xs_base = T * B.pos0 + B.pre_dn;
-  const R* xs = static_cast<const R*>(a.x_save);
+  const R* xs = static_cast<const R*>(a.x_save) + T * B.pos0 + B.pre_dn;
   R* out = static_cast<R*>(a.runoff);
   const R qlb = R(a.c[1]);
+  const int tid = threadIdx.x;
+  if (tid < kTileR) sref[tid] = a.s.ref[B.pos0 + r0 + (tid < nr ? tid : 0)];
   {
-    const int i = threadIdx.x % kTileR;  // reach (fastest: coalesced along the tick row)
-    if (i < nr) {
-      const int off = a.s.off[B.pos0 + r0 + i];
-      for (int j = threadIdx.x / kTileR; j < kTileT; j += 256 / kTileR)
-        if (t0 + j < T) tile[j][i] = xs[xs_base + (t0 + j + off) * B.nloc + r0 + i];
+    const int i = tid % kTileR, j0 = tid / kTileR;  // reach fastest: coalesced along a tick row
+    const int ic = i < nr ? i : 0;
+    const int off = a.s.off[B.pos0 + r0 + ic];
+    R v[kTrPer];
+#pragma unroll
+    for (int m = 0; m < kTrPer; ++m) {
+      int64_t t = t0 + j0 + 4 * m;
+      t = t < T ? t : T - 1;
+      v[m] = xs[(t + off) * B.nloc + r0 + ic];
     }
+#pragma unroll
+    for (int m = 0; m < kTrPer; ++m) tile[j0 + 4 * m][i] = v[m];
   }
   __syncthreads();
-  const int j = threadIdx.x % kTileT;    // step (fastest: coalesced along the reach row)
-  for (int i = threadIdx.x / kTileT; i < nr; i += 256 / kTileT) {
-    if (t0 + j < T) out[(int64_t)a.s.ref[B.pos0 + r0 + i] * T + t0 + j] = rmax(tile[j][i], qlb);
+  const int j = tid % kTileT, i0 = tid / kTileT;  // step fastest: coalesced along a reach row
+  if (t0 + j < T) {
+#pragma unroll
+    for (int m = 0; m < kTrPer; ++m) {
+      const int i = i0 + 4 * m;
+      if (i < nr) out[(int64_t)sref[i] * T + t0 + j] = rmax(tile[j][i], qlb);
+    }
   }
 }
 
@@ -567,34 +585,45 @@ __global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
 template <typename R>
 __global__ void __launch_bounds__(256) expand_grad_kernel(RouteArgs a) {
   __shared__ R tile[kTileT][kTileR + 1];
+  __shared__ int sref[kTileR];
   const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
   const BlockDesc B = a.s.blocks[b];
   const int nr = min(kTileR, B.nloc - r0);
   const int64_t T = a.T;
   const int64_t t0 = (int64_t)blockIdx.y * kTileT;
-  const int64_t xs_base = T * B.pos0 + B.pre_dn;
   const R* go = static_cast<const R*>(a.grad_out);
-  R* gs = static_cast<R*>(a.gs);
+  R* gs = static_cast<R*>(a.gs) + T * B.pos0 + B.pre_dn;
+  const int tid = threadIdx.x;
+  if (tid < kTileR) sref[tid] = a.s.ref[B.pos0 + r0 + (tid < nr ? tid : 0)];
+  __syncthreads();
   {
-    const int j = threadIdx.x % kTileT;
-    for (int i = threadIdx.x / kTileT; i < nr; i += 256 / kTileT) {
-      if (t0 + j >= T) continue;
-      const int64_t ref = a.s.ref[B.pos0 + r0 + i];
-      R g = R(0);
-      if (a.g_roff) {
-        for (int64_t m = a.g_roff[ref]; m < a.g_roff[ref + 1]; ++m) g = g + go[a.g_rg[m] * T + t0 + j];
-      } else {
-        g = go[ref * T + t0 + j];
+    const int j = tid % kTileT, i0 = tid / kTileT;
+    const int64_t tc = t0 + j < T ? t0 + j : T - 1;
+    R v[kTrPer];
+    if (a.g_roff) {
+#pragma unroll
+      for (int m = 0; m < kTrPer; ++m) {
+        const int64_t ref = sref[i0 + 4 * m];
+        R g = R(0);
+        for (int64_t q = a.g_roff[ref]; q < a.g_roff[ref + 1]; ++q) g = g + go[a.g_rg[q] * T + tc];
+        v[m] = g;
       }
-      tile[j][i] = g;
+    } else {
+#pragma unroll
+      for (int m = 0; m < kTrPer; ++m) v[m] = go[(int64_t)sref[i0 + 4 * m] * T + tc];
     }
+#pragma unroll
+    for (int m = 0; m < kTrPer; ++m) tile[j][i0 + 4 * m] = v[m];
   }
   __syncthreads();
-  const int i = threadIdx.x % kTileR;
+  const int i = tid % kTileR, j0 = tid / kTileR;
   if (i < nr) {
     const int off = a.s.off[B.pos0 + r0 + i];
-    for (int j = threadIdx.x / kTileR; j < kTileT; j += 256 / kTileR)
-      if (t0 + j < T) gs[xs_base + (t0 + j + off) * B.nloc + r0 + i] = tile[j][i];
+#pragma unroll
+    for (int m = 0; m < kTrPer; ++m) {
+      const int64_t t = t0 + j0 + 4 * m;
+      if (t < T) gs[(t + off) * B.nloc + r0 + i] = tile[j0 + 4 * m][i];
+    }
   }
 }
 
