@@ -17,6 +17,7 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--reaches 800000] [
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -81,6 +82,34 @@ def cpu_baseline(args):
                       f"spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve), {el:.1f} s"}
 
 
+def block_profile(path, g, step, lib):
+    """One extra step with the per-workgroup profile on: start/end/import-wait per block (µs)."""
+    nb = g.info.n_blocks
+    bufs = [torch.zeros(16 * nb, dtype=torch.int64, device=g.device) for _ in range(2)]
+    for w in (0, 1):
+        lib.ddr_set_block_profile(w, ctypes.c_void_p(bufs[w].data_ptr()))
+    step(False)
+    torch.cuda.synchronize()
+    for w in (0, 1):
+        lib.ddr_set_block_profile(w, None)
+    s = g.structure()
+    sizes = np.bincount(s["block"], minlength=nb)
+    out = {}
+    for w, key in ((0, "forward"), (1, "backward")):
+        p = bufs[w].view(nb, 16).cpu().numpy()
+        t0 = p[:, 0].min()
+        out[key] = {"start_us": ((p[:, 0] - t0) / 100.0).tolist(), "end_us": ((p[:, 1] - t0) / 100.0).tolist(),
+                    "wait_us": (p[:, 2] / 100.0).tolist(), "hwid": (p[:, 3] & 0xFFFFFFFF).tolist(),
+                    "xcc": (p[:, 3] >> 32).tolist(),
+                    "tick1024_us": np.where(p[:, 4:] > 0, (p[:, 4:] - t0) / 100.0, -1).tolist()}
+        e = (p[:, 1] - t0) / 100.0
+        log(f"[profile] {key}: end min/median/max {e.min():.0f}/{np.median(e):.0f}/{e.max():.0f} us, "
+            f"wait max {p[:, 2].max() / 100:.0f} us")
+    out["nloc"] = sizes.tolist()
+    Path(path).parent.mkdir(parents=True, exist_ok=True)
+    Path(path).write_text(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -96,6 +125,7 @@ def main():
     ap.add_argument("--cpu-reaches", type=int, default=20_000)
     ap.add_argument("--cpu-T", type=int, default=240)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -134,6 +164,10 @@ def main():
         return n, q, p
 
     ev = {k: [] for k in ("f0", "f1", "b1")}
+    kms = {"forward": [], "backward": []}  # main routing kernels, HIP events on the launch stream
+    from ddr_amd import _lib
+
+    lib = _lib.load()
 
     def step(record: bool):
         for t_ in (u_n, u_q, u_p):
@@ -153,12 +187,17 @@ def main():
             ev["f0"].append(e0)
             ev["f1"].append(e1)
             ev["b1"].append(e2)
+            for w, key in ((0, "forward"), (1, "backward")):
+                ms = ctypes.c_float()
+                _lib.check(lib.ddr_kernel_ms(w, ctypes.byref(ms)))
+                kms[key].append(ms.value)
         return runoff
 
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs resident ({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB); warmup {args.warmup}")
     for _ in range(args.warmup):
         step(False)
+    _lib.check(lib.ddr_set_kernel_timing(1))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -172,6 +211,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    _lib.check(lib.ddr_set_kernel_timing(0))
+    if args.block_profile and rank == 0:
+        block_profile(args.block_profile, g, step, lib)
     fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["f0"], ev["f1"])]))
     bwd_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["f1"], ev["b1"])]))
     local = torch.tensor([float(net.n)], device=dev, dtype=torch.float64)
@@ -184,9 +226,10 @@ def main():
     value = total_reaches * (T - 1) * args.steps / elapsed
     if rank == 0:
         reach_steps = net.n * (T - 1)
-        kern = {"forward": {"ms": fwd_ms, "GB/s": FWD_BYTES * reach_steps / (fwd_ms * 1e-3) / 1e9},
-                "backward": {"ms": bwd_ms, "GB/s": BWD_BYTES * reach_steps / (bwd_ms * 1e-3) / 1e9}}
-        dom = "backward" if bwd_ms >= fwd_ms else "forward"
+        kf, kb = float(np.mean(kms["forward"])), float(np.mean(kms["backward"]))
+        kern = {"forward": {"op_ms": fwd_ms, "kernel_ms": kf, "GB/s": FWD_BYTES * reach_steps / (kf * 1e-3) / 1e9},
+                "backward": {"op_ms": bwd_ms, "kernel_ms": kb, "GB/s": BWD_BYTES * reach_steps / (kb * 1e-3) / 1e9}}
+        dom = "backward" if kb >= kf else "forward"
         achieved = kern[dom]["GB/s"]
         cpu = None if args.no_cpu_baseline else cpu_baseline(args)
         out = {

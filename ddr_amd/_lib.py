@@ -39,7 +39,7 @@ DDR_FWD_NO_RUNOFF = 4
 
 class BuildOpts(C.Structure):
     _fields_ = [("flags", C.c_int32), ("max_block_reaches", C.c_int32), ("target_blocks", C.c_int32),
-                ("max_resident", C.c_int32)]
+                ("max_resident", C.c_int32), ("steps_hint", C.c_int32)]
 
 
 class GraphInfo(C.Structure):
@@ -88,6 +88,9 @@ _SIGS = {
     "ddr_graph_status": (C.c_int, [_P, _P]),
     "ddr_tri_solve": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _P]),
     "ddr_tri_grad_values": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P]),
+    "ddr_set_kernel_timing": (C.c_int, [_I32]),
+    "ddr_kernel_ms": (C.c_int, [_I32, C.POINTER(C.c_float)]),
+    "ddr_set_block_profile": (C.c_int, [_I32, _P]),
     "ddr_device_info": (C.c_int, [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "ddr_last_error": (C.c_char_p, []),
     "ddr_version": (C.c_char_p, []),

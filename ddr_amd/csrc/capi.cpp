@@ -31,6 +31,26 @@ using namespace ddr;
 
 namespace {
 
+// Measurement hooks (ddr_set_kernel_timing / ddr_set_block_profile): process-wide, not for
+// concurrent use from several host threads.
+struct KernelTiming {
+  bool on = false;
+  hipEvent_t ev[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  bool recorded[2] = {false, false};
+} g_timing;
+unsigned long long* g_prof[2] = {nullptr, nullptr};
+
+hipError_t timing_mark(int which, int edge, hipStream_t s) {
+  if (!g_timing.on) return hipSuccess;
+  hipEvent_t& e = g_timing.ev[which][edge];
+  if (!e) {
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) return r;
+  }
+  if (edge == 1) g_timing.recorded[which] = true;
+  return hipEventRecord(e, s);
+}
+
 template <typename R>
 ddr_status check_common(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, int64_t T) {
   if (!gh || !c || !r) return fail(DDR_ERR_ARG, "null graph/consts/reaches");
@@ -108,7 +128,12 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   a.q_last = q_last;
   a.tw_last = tw;
   a.ss_last = ss;
+  a.prof = g_prof[0];
+  a.qs = x_save + (g->n * T + g->sum_dn);
+  DDR_HIP(launch_gather_qprime<R>(g, a, s));
+  DDR_HIP(timing_mark(0, 0, s));
   DDR_HIP(launch_route<R>(g, a, false, s));
+  DDR_HIP(timing_mark(0, 1, s));
   if (runoff && !(flags & DDR_FWD_NO_RUNOFF)) DDR_HIP(launch_emit_runoff<R>(g, a, s));
   return DDR_OK;
 }
@@ -134,6 +159,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   RouteArgs a;
   fill_common<R>(a, g, c, r, T, qprime, flags);
   a.x_save = const_cast<R*>(x_save);
+  a.qs = const_cast<R*>(x_save) + (g->n * T + g->sum_dn);
   a.bnd = const_cast<double*>(bnd);
   a.status = static_cast<unsigned*>(status);
   a.grad_out = grad;
@@ -145,8 +171,11 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   a.gp = gp;
   // workspace: [2 n_cut T f64 boundary][3 N f64 accumulators][grad in the schedule layout (R)]
   a.gs = bwd_bnd + 2 * g->n_cut * T + 3 * g->n;
+  a.prof = g_prof[1];
   DDR_HIP(launch_expand_grad<R>(g, a, s));
+  DDR_HIP(timing_mark(1, 0, s));
   DDR_HIP(launch_route<R>(g, a, true, s));
+  DDR_HIP(timing_mark(1, 1, s));
   return DDR_OK;
 }
 
@@ -215,8 +244,8 @@ ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
   info->max_depth = g->max_depth;
   info->max_block_depth = g->max_block_depth;
   info->reaches_per_thread = g->kr;
-  info->save_elems_per_t = g->n;
-  info->save_elems_fixed = g->sum_dn;
+  info->save_elems_per_t = 2 * g->n;  // x (routing states) | q' gathered into the same layout
+  info->save_elems_fixed = 2 * g->sum_dn;
   info->bnd_elems_per_t = g->n_cut;
   info->bwd_elems_per_t = 2 * g->n_cut;
   info->bwd_elems_fixed = 3 * g->n;
@@ -283,6 +312,25 @@ ddr_status ddr_graph_status(const void* status, void* stream) {
   DDR_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   if (h[0]) return fail(DDR_ERR_TIMEOUT, std::to_string(h[0]) + " inter-workgroup hand-offs timed out (first block " +
                                              std::to_string((int)h[1] - 1) + ")");
+  return DDR_OK;
+}
+
+ddr_status ddr_set_kernel_timing(int32_t enable) {
+  g_timing.on = enable != 0;
+  return DDR_OK;
+}
+
+ddr_status ddr_kernel_ms(int32_t which, float* ms) {
+  if ((which != 0 && which != 1) || !ms) return fail(DDR_ERR_ARG, "bad ddr_kernel_ms arguments");
+  if (!g_timing.recorded[which]) return fail(DDR_ERR_ARG, "no timed launch recorded");
+  DDR_HIP(hipEventSynchronize(g_timing.ev[which][1]));
+  DDR_HIP(hipEventElapsedTime(ms, g_timing.ev[which][0], g_timing.ev[which][1]));
+  return DDR_OK;
+}
+
+ddr_status ddr_set_block_profile(int32_t which, uint64_t* buf) {
+  if (which != 0 && which != 1) return fail(DDR_ERR_ARG, "which must be 0 or 1");
+  g_prof[which] = reinterpret_cast<unsigned long long*>(buf);
   return DDR_OK;
 }
 

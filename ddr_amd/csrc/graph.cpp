@@ -13,6 +13,8 @@
 // one tick ("as late as possible" wavefront).  Large basins are split into connected pieces whose
 // inter-piece edges become cut edges exchanged through global memory.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <memory>
 #include <numeric>
@@ -106,29 +108,61 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   int64_t target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu) * kBlocksPerCU;
   resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
   int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + target - 1) / target));
+  const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
 
-  std::vector<int64_t> piece(n), resid(n), dloc_piece(n);
+  // Splitting works on full-subtree sizes and heights: sub(i) = reaches draining through i,
+  // ht(i) = longest path from i up to a source.
+  std::vector<int64_t> sub(n, 1), ht(n, 0);
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
+      sub[i] += sub[col[k]];
+      ht[i] = std::max(ht[i], ht[col[k]] + 1);
+    }
+  std::vector<int64_t> piece(n), resid(n), stem(n), dloc_piece(n);
   std::vector<char> is_root(n);
   std::vector<Piece> pieces;
+  std::vector<int64_t> others;
   for (;;) {
+    // Stem-preserving split (bottom-up).  A reach whose subtree exceeds the capacity keeps its
+    // deepest child (the main stem: every block boundary crossed along the longest flow path adds
+    // a hand-off to the critical path) and absorbs other children, smallest first, while the
+    // piece's tributary mass stays within cap - lseg, so every piece carries a stem stretch of at
+    // least lseg reaches.  The stem child is cut only when the piece is full.
+    // Pieces of split basins are kept below the block capacity: they land in blocks on long
+    // chains, whose packing weight is up to ~(T + depth) / T times their size.
+    const int64_t scap = cap * 4 / 5;
+    const int64_t lseg = scap / 8;
     std::fill(is_root.begin(), is_root.end(), 0);
     for (int64_t i = 0; i < n; ++i) {
-      int64_t total = 1;
-      for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) total += resid[col[k]];
-      if (bsize[g->basin[i]] > cap) {
-        // cut the heaviest remaining children until this reach's residual subtree fits
-        while (total > cap) {
-          int64_t best = -1;
-          for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
-            int64_t c = col[k];
-            if (!is_root[c] && (best < 0 || resid[c] > resid[best])) best = c;
-          }
-          if (best < 0) break;
-          is_root[best] = 1;
-          total -= resid[best];
-        }
+      const int64_t k0 = cnt[i], k1 = cnt[i + 1];
+      if (sub[i] <= scap || k0 == k1) {
+        resid[i] = sub[i];
+        stem[i] = ht[i] + 1;
+        continue;
       }
-      resid[i] = total;
+      int64_t dc = col[k0];
+      for (int64_t k = k0 + 1; k < k1; ++k) {
+        const int64_t c = col[k];
+        if (ht[c] > ht[dc] || (ht[c] == ht[dc] && sub[c] > sub[dc])) dc = c;
+      }
+      int64_t base = 1 + resid[dc], trib = resid[dc] - stem[dc];
+      const bool keep = base <= scap;
+      if (!keep) {
+        is_root[dc] = 1;
+        base = 1;
+        trib = 0;
+      }
+      others.clear();
+      for (int64_t k = k0; k < k1; ++k)
+        if (col[k] != dc) others.push_back(col[k]);
+      std::stable_sort(others.begin(), others.end(), [&](int64_t a, int64_t b) { return resid[a] < resid[b]; });
+      int64_t acc = 0;
+      for (int64_t c : others) {
+        if (trib + acc + resid[c] <= scap - lseg && base + acc + resid[c] <= scap) acc += resid[c];
+        else is_root[c] = 1;
+      }
+      resid[i] = base + acc;
+      stem[i] = keep ? 1 + stem[dc] : 1;
     }
     pieces.clear();
     for (int64_t i = n - 1; i >= 0; --i) {
@@ -158,36 +192,74 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     }
     int64_t ncut = 0;
     for (auto& P : pieces) ncut += (g->down[P.root] >= 0);
-    // first-fit-decreasing packing of pieces of equal height into blocks of capacity cap
-    std::vector<int64_t> order(pieces.size());
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-      if (pieces[a].height != pieces[b].height) return pieces[a].height < pieces[b].height;
-      return pieces[a].size > pieces[b].size;
-    });
-    std::vector<int64_t> block_of_piece(pieces.size());
-    std::vector<int64_t> load;   // per block
-    std::vector<int64_t> bheight;
-    size_t hstart = 0;  // first block of the current height class
-    int64_t curh = -1;
-    for (int64_t p : order) {
-      if (pieces[p].height != curh) {
-        curh = pieces[p].height;
-        hstart = load.size();
+    // Packing: pieces of equal height share blocks (so the block dependency graph is a DAG),
+    // worst-fit by weight.  A block on a long inter-block chain starts late (forward: blocks near
+    // the outlet wait for the chain above them; backward: blocks near the sources) and runs
+    // T + lag ticks, so pieces are weighted by (T + lag + dmax) / T of the block they landed in and
+    // the packing is repeated: long-chain blocks get fewer reaches and tick faster.
+    std::vector<double> w(pieces.size()), F;
+    for (size_t p = 0; p < pieces.size(); ++p) w[p] = (double)pieces[p].size;
+    std::vector<int64_t> order(pieces.size()), block_of_piece(pieces.size()), load, bdm;
+    std::vector<double> wload;
+    for (int it = 0; it < 3; ++it) {
+      double wsum = 0.0;
+      for (double x : w) wsum += x;
+      const double capw = (double)cap * wsum / (double)n;  // the unweighted cap, scaled by the mean weight
+      std::iota(order.begin(), order.end(), 0);
+      std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        if (pieces[a].height != pieces[b].height) return pieces[a].height < pieces[b].height;
+        return w[a] > w[b];
+      });
+      load.clear();
+      wload.clear();
+      size_t hstart = 0;  // first block of the current height class
+      int64_t curh = -1;
+      for (int64_t p : order) {
+        if (pieces[p].height != curh) {
+          curh = pieces[p].height;
+          hstart = load.size();
+        }
+        int64_t best = -1;
+        for (size_t b = hstart; b < load.size(); ++b)
+          if (wload[b] + w[p] <= capw * 1.0001 && load[b] + pieces[p].size <= hard_cap &&
+              (best < 0 || wload[b] < wload[best]))
+            best = (int64_t)b;
+        if (best < 0) {
+          best = (int64_t)load.size();
+          load.push_back(0);
+          wload.push_back(0.0);
+        }
+        load[best] += pieces[p].size;
+        wload[best] += w[p];
+        block_of_piece[p] = best;
       }
-      int64_t best = -1;
-      // worst-fit among open blocks of this height keeps loads balanced (LPT-like)
-      for (size_t b = hstart; b < load.size(); ++b)
-        if (load[b] + pieces[p].size <= cap && (best < 0 || load[b] < load[best])) best = (int64_t)b;
-      if (best < 0) {
-        best = (int64_t)load.size();
-        load.push_back(0);
-        bheight.push_back(curh);
+      // block lags (ticks) along the block DAG, per cut edge p -> c:
+      //   forward  lagf(c) >= lagf(p) + dmax(p) - dmax(c) + dist_in_piece(d) + 1 + kChunk
+      //   backward lagb(p) >= lagb(c) + dist_in_piece(d) + kChunk
+      const size_t nb = load.size();
+      bdm.assign(nb, 0);
+      for (size_t p = 0; p < pieces.size(); ++p) bdm[block_of_piece[p]] = std::max(bdm[block_of_piece[p]], pieces[p].dmax);
+      std::vector<int64_t> lagf(nb, 0), lagb(nb, 0);
+      for (int sweep = 0; sweep < 1000; ++sweep) {
+        bool changed = false;
+        for (size_t p = 0; p < pieces.size(); ++p) {
+          const int64_t d = g->down[pieces[p].root];
+          if (d < 0) continue;
+          const int64_t pb = block_of_piece[p], cb = block_of_piece[piece[d]];
+          const int64_t lf = lagf[pb] + bdm[pb] - bdm[cb] + dloc_piece[d] + 1 + kChunk;
+          if (lf > lagf[cb]) { lagf[cb] = lf; changed = true; }
+          const int64_t lb = lagb[cb] + dloc_piece[d] + kChunk;
+          if (lb > lagb[pb]) { lagb[pb] = lb; changed = true; }
+        }
+        if (!changed) break;
       }
-      load[best] += pieces[p].size;
-      block_of_piece[p] = best;
+      F.assign(nb, 1.0);
+      for (size_t b = 0; b < nb; ++b)
+        F[b] = (steps + (double)std::max(lagf[b], lagb[b]) + (double)bdm[b]) / steps;
+      for (size_t p = 0; p < pieces.size(); ++p) w[p] = (double)pieces[p].size * F[block_of_piece[p]];
     }
     const int64_t nblocks = (int64_t)load.size();
+    if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part] cap %ld hard %ld pieces %zu blocks %ld cut %ld\n", (long)cap, (long)hard_cap, pieces.size(), (long)nblocks, (long)ncut);
     {
       // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if two
       // workgroups would no longer fit on a CU
@@ -206,6 +278,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
         mc = std::max(mc, bc[b]);
       }
       const size_t need = std::max(route_lds_bytes(ms, mv, false, 4), route_lds_bytes(ms, mc, true, 4));
+      if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld lds %zu\n", (long)ms, (long)mv, (long)mc, need);
       if (need > kLdsBudget) {
         if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
         hard_cap -= hard_cap / 8;
@@ -219,7 +292,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
                                           " co-resident workgroups but the device admits " +
                                           std::to_string(resident));
       }
-      cap = std::min<int64_t>(hard_cap, cap + cap / 4 + 1);
+      cap = std::min<int64_t>(hard_cap, cap + cap / 32 + 1);
       continue;
     }
     // ---- emit the schedule ---------------------------------------------------------------
@@ -305,6 +378,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       if (dl[P] == -2) dl[P] = (int32_t)local[g->down[i]];
     }
     g->sum_dn = pre_dn;
+    g->max_nloc = (int)max_load;
     int kr = 1;
     while (int64_t(kr) * bs < max_load) kr *= 2;
     g->kr = kr;
@@ -333,6 +407,20 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     }
     if ((st = upload(g.get(), &D.pos_of_ref, pos_of_ref))) return st;
     if ((st = upload(g.get(), &D.block_of_pos, block_of_pos))) return st;
+    // per block: local indices in ascending reference order (coalesced reads of q' rows)
+    std::vector<int32_t> rs_loc(n), rs_ref(n);
+    for (int64_t b = 0; b < nblocks; ++b) {
+      const BlockDesc& B = g->blocks[b];
+      std::vector<std::pair<int32_t, int32_t>> v(B.nloc);
+      for (int32_t r = 0; r < B.nloc; ++r) v[r] = {ref[B.pos0 + r], r};
+      std::sort(v.begin(), v.end());
+      for (int32_t k = 0; k < B.nloc; ++k) {
+        rs_ref[B.pos0 + k] = v[k].first;
+        rs_loc[B.pos0 + k] = v[k].second;
+      }
+    }
+    if ((st = upload(g.get(), &D.rs_loc, rs_loc))) return st;
+    if ((st = upload(g.get(), &D.rs_ref, rs_ref))) return st;
     std::vector<int32_t> rtile;
     for (int64_t b = 0; b < nblocks; ++b)
       for (int32_t r0 = 0; r0 < g->blocks[b].nloc; r0 += kTileR) {

@@ -12,18 +12,30 @@
 
 namespace ddr {
 
-// Routing workgroups: 512 threads, up to kMaxKR reaches per thread, two workgroups per CU
-// (4 waves per SIMD: the per-reach statics live in LDS, not registers, so the 128-VGPR budget of
-// that occupancy holds KR = 4).
-constexpr int kBlockThreads = 512;
+// Routing workgroups: 1024 threads (16 waves, 4 per SIMD), one per CU, up to kMaxKR reaches per
+// thread.  The per-reach statics live in LDS, not registers, so the 128-VGPR budget of 4 waves per
+// SIMD holds KR = 4.  One workgroup per CU (not two of 512): co-resident workgroups are served by
+// age priority, so the younger one of a pair progresses at less than half the older one's tick
+// rate, and every multi-workgroup basin is throttled to its slowest member (measured).
+#ifndef DDR_BLOCK_THREADS
+#define DDR_BLOCK_THREADS 1024
+#endif
+constexpr int kBlockThreads = DDR_BLOCK_THREADS;
 constexpr int kMaxKR = 4;
-constexpr int kBlocksPerCU = 2;
-// Default workgroup capacity (reaches): leaves LDS room for virtual inflows at two blocks per CU.
-constexpr int kDefaultBlockReaches = 1920;
-// LDS budget per workgroup for two per CU (160 KiB per CU).
+constexpr int kBlocksPerCU = 1024 / kBlockThreads;
+// Default workgroup capacity (reaches), leaving LDS room for virtual inflows.
+constexpr int kDefaultBlockReaches = kBlockThreads * 15 / 4;
+// LDS budget per workgroup (160 KiB per CU).
 constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
-// Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").
-constexpr int kChunk = 32;
+// Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").  Every
+// block-DAG hop adds about one chunk of lag, so the chunk is short.
+#ifndef DDR_CHUNK
+#define DDR_CHUNK 8
+#endif
+constexpr int kChunk = DDR_CHUNK;
+// Parameter-gradient partial sums are flushed to the fp64 accumulators every kGradFlush steps
+// (aligned to the step index, so the summation grouping does not depend on the partition).
+constexpr int kGradFlush = 32;
 // Transpose tiles between the (reach, step) layouts of the API and the tick-major schedule layout.
 constexpr int kTileR = 64;
 constexpr int kTileT = 64;
@@ -71,6 +83,8 @@ struct DevSchedule {
   int32_t* pos_of_ref = nullptr;   // (N) internal position of each reference reach
   int32_t* block_of_pos = nullptr; // (N) block of each internal position
   int32_t* rtile = nullptr;        // (n_rtiles, 2) tiles of kTileR reaches: (block, first local index)
+  int32_t* rs_loc = nullptr;       // (N) per block, local indices in ascending reference order
+  int32_t* rs_ref = nullptr;       // (N) the matching reference indices
 };
 
 struct Graph {
@@ -84,6 +98,7 @@ struct Graph {
   int device = 0;
   std::vector<BlockDesc> blocks;
   int64_t sum_dn = 0;    // sum over blocks of dmax * nloc
+  int max_nloc = 0;      // largest block
   int64_t n_rtiles = 0;  // tiles of kTileR reaches (never straddling a block) for the layout transposes
   DevSchedule dev;
   std::vector<void*> allocations;

@@ -103,6 +103,26 @@ __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
 __device__ __forceinline__ int up_0(unsigned u) { return (int)(u & 8191u); }
 __device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u); }
 
+// Debug per-workgroup profile (ddr_set_block_profile): start, end, import wait, hardware id.
+// Layout per workgroup: kProfWords uint64 = start, end, wait, hwid, then a timestamp every 1024 ticks.
+constexpr int kProfWords = 16;
+__device__ __forceinline__ void prof_begin(unsigned long long* p) {
+  p += kProfWords * blockIdx.x;
+  p[0] = __builtin_amdgcn_s_memrealtime();
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  p[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+}
+__device__ __forceinline__ void prof_tick(unsigned long long* p, int tick) {
+  if ((tick & 1023) == 0 && (tick >> 10) < kProfWords - 4)
+    p[kProfWords * blockIdx.x + 4 + (tick >> 10)] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void prof_end(unsigned long long* p, unsigned long long wait) {
+  p += kProfWords * blockIdx.x;
+  p[1] = __builtin_amdgcn_s_memrealtime();
+  p[2] = wait;
+}
+
 }  // namespace
 
 // Per-reach statics in LDS: six arrays of S reals (n, qe, p, sqrtS, L, X).  The derived fields
@@ -140,6 +160,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
+  // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
+  // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
@@ -147,17 +170,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
-  const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
   R* xsave = static_cast<R*>(a.x_save);
-  const R* qp = static_cast<const R*>(a.qprime);
+  const int TTf = (int)T + B.dmax;
   const R* q0p = static_cast<const R*>(a.q0);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
 
   int ref[KR], off[KR];
   unsigned up[KR];
   bool cut[KR];
-  R Q[KR], In[KR], fsr[KR], qa[KR], qb[KR];
+  R Q[KR], In[KR], qa[KR], qb[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -167,7 +189,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     off[k] = a.s.off[P];
     up[k] = pack_up(a, P);
     cut[k] = a.s.cut[P] >= 0;
-    fsr[k] = a.fs ? static_cast<const R*>(a.fs)[ref[k]] : R(1);  // mmc.py:303-304 (q' * flow_scale)
     Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
     if (hk) tab.put(r, load_static<R>(a, ref[k]));
@@ -177,16 +198,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if (vown) v_off = a.s.v_off[B.virt0 + tid];
   load_math_tables();
   __syncthreads();
+  unsigned long long prof_wait = 0;
+  if (a.prof && tid == 0) prof_begin(a.prof);
 
-  // q'[max(t-1,0)] (or the carried Q0 at t = 0) for the step each reach runs at tick `tau`
-  auto prefetch = [&](int tau, R(&dst)[KR]) {
+  // q'[max(t-1,0)] * flow_scale (gathered into the schedule layout: one row per tick), or the
+  // carried Q0 at t = 0, for the step each reach runs at tick `tau`
+  const R* qsb = static_cast<const R*>(a.qs) + xs_base;
+  auto prefetch = [&](int tau, R(&dst)[KR], int tq0) {
+    const R* row = qsb + (int64_t)(tau < TTf ? tau : TTf - 1) * B.nloc;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      const int tn = tau - off[k];
-      int64_t row = tn - 1;
-      row = row < 0 ? 0 : (row >= T ? T - 1 : row);
-      const R* src = (carry && tn == 0) ? (q0p + ref[k]) : (qp + row * N + ref[k]);
-      dst[k] = *src;
+      if (wbase + k * BS >= B.nloc) continue;
+      const int r = tq0 + k * BS;
+      dst[k] = (carry && tau == off[k]) ? q0p[ref[k]] : row[r < B.nloc ? r : 0];
     }
   };
 
@@ -199,10 +223,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       ref[k] = opq(ref[k]);
       off[k] = opq(off[k]);
       up[k] = opq(up[k]);
-      fsr[k] = opq(fsr[k]);
     }
     if (B.nvirt > 0 && (tau % kChunk) == 0) {
       // import the next chunk of every virtual inflow (x of the upstream block's reach)
+      const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
       for (int w = tid; w < B.nvirt * kChunk; w += BS) {
         const int v = w / kChunk, sidx = w % kChunk;
         const int e = a.s.v_edge[B.virt0 + v];
@@ -212,18 +236,20 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         ring[v * kChunk + sidx] = val;
       }
       lds_barrier();
+      if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
-    prefetch(tau + 1, qnext);
+    prefetch(tau + 1, qnext, tq);
     double xk[KR];
     // ---- compute: one reach at a time (gather, physics, fp64 column sweep) -------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       const bool hk = r < B.nloc;
       const int t = tau - off[k];
       const int nup = up_n(up[k]);
       const ReachStatic<R> st = tab.get(hk ? r : 0);
-      const R qv = qcur[k] * fsr[k];
+      const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
       R c1, c2, c3, c4, tw, ss;
       coefficients<R>(st, Q[k], cs, c1, c2, c3, c4, tw, ss);
       const R qc = rmax(qv, cs.qlb);                                  // mmc.py:421-424
@@ -280,6 +306,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // ---- publish ------------------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
       const int t = tau - off[k];
       const int r = tq + k * BS;
       if (r < B.nloc && t >= 0 && t < T) sx[r] = xk[k];
@@ -292,14 +319,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   const int TT = (int)T + B.dmax;
-  prefetch(0, qa);
+  prefetch(0, qa, tid);
   // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
 #pragma unroll 1
   for (int tau = 0; tau < TT; ++tau) {
+    if (a.prof && tid == 0) prof_tick(a.prof, tau);
     tick(tau, qa, qb);
 #pragma unroll
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
+  if (a.prof && tid == 0) prof_end(a.prof, prof_wait);
 }
 
 // ============================================================================================
@@ -315,6 +344,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   constexpr int BS = kBlockThreads;
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
+  // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
+  // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
+  const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sa = reinterpret_cast<double*>(smem + kMathTabBytes);  // [S] c1_i * gb_i  (fp64, transposed solve)
@@ -323,11 +355,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
-  const int64_t N = a.N;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const R* xsave = static_cast<const R*>(a.x_save);
   const R* gsch = static_cast<const R*>(a.gs);
-  const R* qp = static_cast<const R*>(a.qprime);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
 
@@ -354,7 +384,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k)
       if (tid + k * BS == loc) dl[k] = -(c + 2);
   }
-  const R* fs = static_cast<const R*>(a.fs);
+  const R* qsb = static_cast<const R*>(a.qs) + xs_base;  // q' * flow_scale, schedule layout
   const bool vown = tid < B.nvirt;
   int v_edge = 0, v_off = 0, v_dloc = 0;
   if (vown) {
@@ -365,12 +395,15 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int TT = (int)T + B.dmax;
   load_math_tables();
   __syncthreads();
+  unsigned long long prof_wait = 0;
+  if (a.prof && tid == 0) prof_begin(a.prof);
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
   auto load_own = [&](int tau, R(&dst)[KR], int tq) {
     const int tc = tau < 0 ? 0 : (tau >= TT ? TT - 1 : tau);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + (r < B.nloc ? r : 0)];
     }
@@ -397,6 +430,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       dl[k] = opq(dl[k]);
     }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
+      const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
       for (int w = tid; w < B.ncout * kChunk; w += BS) {
         const int c = w / kChunk, sidx = w % kChunk;
         const int P = B.pos0 + a.s.cout_loc[B.cout0 + c];
@@ -411,6 +445,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         ring[(c * kChunk + sidx) * 2 + 1] = Bv;
       }
       lds_barrier();
+      if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     // ---- read ---------------------------------------------------------------------------------
     if (vown) {
@@ -427,6 +462,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k) {
       A[k] = 0.0;
       Bd[k] = R(0);
+      if (wbase + k * BS >= B.nloc) continue;
       if (dl[k] >= 0) {
         A[k] = sa[dl[k]];
         Bd[k] = sb[dl[k]];
@@ -442,6 +478,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     //      geometry recompute, which hides their latency) ------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       const bool hk = r < B.nloc;
       const int rs = hk ? r : 0;
@@ -450,14 +487,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
       const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + rs];  // own x(t)
       const R gk = gsch[xs_base + (int64_t)tau * B.nloc + rs];    // dL/dQ_t (expand_grad_kernel)
-      const R qv0 = qp[(tcl >= 1 ? tcl - 1 : 0) * N + ref[k]];
+      const R qvk = qsb[(int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale (mmc.py:303-304)
       const R xu0 = up_x(up_0(up[k]), tau - 1, tcl);
       const R xu1 = up_x(up_1(up[k]), tau - 1, tcl);
       const R xup0 = up_x(up_0(up[k]), tau - 2, tcl - 1);
       const R xup1 = up_x(up_1(up[k]), tau - 2, tcl - 1);
       const ReachStatic<R> st = tab.template get<true>(rs);
-      R qvk = qv0;
-      if (fs) qvk = qvk * fs[ref[k]];                    // mmc.py:303-304
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
       const double gb64 = (double)gx + A[k];             // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
@@ -491,10 +526,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         pn[k] = pn[k] + gn;
         pq[k] = pq[k] + gq;
         pp[k] = pp[k] + gp;
-        // flush the fp32 partial sums into the fp64 accumulators every kChunk *steps* (aligned to
+        // flush the fp32 partial sums into the fp64 accumulators every kGradFlush *steps* (aligned to
         // t, not to ticks, so the summation grouping -- and the result -- is independent of the
         // partition); one owner per address, so the atomics are deterministic
-        if ((t % kChunk) == 1 || t == 1) {
+        if ((t % kGradFlush) == 1 || t == 1) {
           double* g3 = gacc + (int64_t)ref[k] * 3;
           atomicAdd(g3 + 0, (double)pn[k]);
           atomicAdd(g3 + 1, (double)pq[k]);
@@ -514,10 +549,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   load_own(TT - 2, xa, tid);
 #pragma unroll 1
   for (int tb = 0; tb < TT; ++tb) {
+    if (a.prof && tid == 0) prof_tick(a.prof, tb);
     tick(tb, xa, xb);
 #pragma unroll
     for (int k = 0; k < KR; ++k) xa[k] = xb[k];
   }
+  if (a.prof && tid == 0) prof_end(a.prof, prof_wait);
 }
 
 // Final fp64 accumulators -> R gradients (reference order).
@@ -539,6 +576,57 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
 // is consumed (memory-level parallelism), and the tile's reference ids are staged in LDS so the
 // scattered side has no dependent global loads.
 constexpr int kTrPer = kTileR * kTileT / 256;
+
+// q'[max(t-1, 0), ref] * flow_scale[ref] -> qs[tick(t, r)] (mmc.py:303-304, 421-424): the routing
+// kernels then read one contiguous row per tick instead of scattered 4-byte values of q' rows.
+// One workgroup per (block, tile of gather_steps steps): reads walk the block's reaches in
+// ascending reference order (runs of adjacent q' columns), writes walk positions (sorted by tick
+// offset, so runs of one offset are contiguous in a tick row); the tile is staged in LDS.
+template <typename R, int G>
+__global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
+  R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
+  const BlockDesc B = a.s.blocks[blockIdx.x];
+  const int64_t T = a.T, N = a.N;
+  const int64_t t0 = (int64_t)blockIdx.y * G;
+  const int nl = B.nloc;
+  const R* qp = static_cast<const R*>(a.qprime);
+  const R* fs = static_cast<const R*>(a.fs);
+  const int* rs_loc = a.s.rs_loc + B.pos0;
+  const int* rs_ref = a.s.rs_ref + B.pos0;
+  int64_t rowoff[G];  // q' row of step t0 + j: max(t - 1, 0), clamped into [0, T)
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    int64_t t = t0 + j;
+    t = t < T ? t : T - 1;
+    rowoff[j] = (t > 0 ? t - 1 : 0) * N;
+  }
+  // all G loads of a reach are independent and issued together (memory-level parallelism)
+#pragma unroll 2
+  for (int i = threadIdx.x; i < nl; i += 1024) {
+    const int ref = rs_ref[i], loc = rs_loc[i];
+    R v[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) v[j] = qp[rowoff[j] + ref];
+    if (fs) {
+      const R f = fs[ref];
+#pragma unroll
+      for (int j = 0; j < G; ++j) v[j] = v[j] * f;
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) tile[j * nl + loc] = v[j];
+  }
+  __syncthreads();
+  R* qs = static_cast<R*>(a.qs) + T * B.pos0 + B.pre_dn;
+  const int* off = a.s.off + B.pos0;
+  const int jn = (int)(T - t0 < G ? T - t0 : G);
+  for (int r = threadIdx.x; r < nl; r += 1024) {
+    const int64_t o = off[r];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (j < jn) qs[(t0 + j + o) * nl + r] = tile[j * nl + r];
+  }
+}
 
 // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
 template <typename R>
@@ -717,6 +805,20 @@ hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t st
 }
 
 template <typename R>
+hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream) {
+  if (g->max_nloc == 0 || a.T == 0) return hipSuccess;
+  constexpr int G = sizeof(R) == 4 ? 8 : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
+  a.gather_steps = G;
+  const size_t smem = (size_t)G * g->max_nloc * sizeof(R);
+  auto kern = gather_qprime_kernel<R, G>;
+  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + G - 1) / G));
+  hipLaunchKernelGGL(kern, grid, dim3(1024), smem, stream, a);
+  return hipGetLastError();
+}
+
+template <typename R>
 hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream) {
   if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
   const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + kTileT - 1) / kTileT));
@@ -740,6 +842,8 @@ template int max_resident_blocks<float>(const Graph*, bool);
 template int max_resident_blocks<double>(const Graph*, bool);
 template hipError_t launch_emit_runoff<float>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_emit_runoff<double>(const Graph*, const RouteArgs&, hipStream_t);
+template hipError_t launch_gather_qprime<float>(const Graph*, RouteArgs&, hipStream_t);
+template hipError_t launch_gather_qprime<double>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_expand_grad<float>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_expand_grad<double>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_gauge<float>(const GaugeArgs&, const float*, float*, hipStream_t);

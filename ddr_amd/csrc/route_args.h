@@ -24,6 +24,8 @@ struct RouteArgs {
   const void* q0;
   void* runoff;
   void* x_save;
+  void* qs;              // lateral inflow in the schedule layout (second half of the x_save workspace)
+  int32_t gather_steps;  // steps per gather_qprime_kernel tile
   double* bnd;
   unsigned* status;
   void* q_last;
@@ -38,6 +40,7 @@ struct RouteArgs {
   void* gn;
   void* gq;
   void* gp;
+  unsigned long long* prof;  // debug per-workgroup profile (ddr_set_block_profile), or null
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
   float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
 };
@@ -60,6 +63,8 @@ template <typename R>
 int max_resident_blocks(const Graph* g, bool backward);
 template <typename R>
 hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream);
+template <typename R>
+hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream);
 template <typename R>
 hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream);
 template <typename R>

@@ -80,14 +80,14 @@ class RiverGraph:
     """Validated, partitioned river network uploaded to the current HIP device."""
 
     def __init__(self, n: int, rows, cols, *, max_block_reaches: int = 0, target_blocks: int = 0,
-                 max_resident: int = 0, host_only: bool = False, device=None):
+                 max_resident: int = 0, steps_hint: int = 0, host_only: bool = False, device=None):
         lib = _lib.load()
         rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
         cols = np.ascontiguousarray(np.asarray(cols, dtype=np.int32))
         if rows.shape != cols.shape:
             raise ValueError("rows and cols must have the same length")
         opts = _lib.BuildOpts(_lib.DDR_BUILD_HOST_ONLY if host_only else 0, int(max_block_reaches),
-                              int(target_blocks), int(max_resident))
+                              int(target_blocks), int(max_resident), int(steps_hint))
         handle = C.c_void_p()
         self._handle = None
         self.host_only = host_only
@@ -156,7 +156,12 @@ class RiverGraph:
         return out
 
     def save_numel(self, T: int) -> int:
+        """Forward workspace (reals): routing states, then q' in the same schedule layout."""
         return self.info.save_elems_per_t * T + self.info.save_elems_fixed
+
+    def state_numel(self, T: int) -> int:
+        """Reals of one schedule-layout (T, N) array (half of :meth:`save_numel`)."""
+        return self.save_numel(T) // 2
 
     def bnd_numel(self, T: int) -> int:
         return self.info.bnd_elems_per_t * T
@@ -164,7 +169,7 @@ class RiverGraph:
     def bwd_numel(self, T: int, itemsize: int = 4) -> int:
         """Backward workspace in doubles: boundary + accumulators, then the gradient expanded to
         the x_save layout in reals of ``itemsize`` bytes."""
-        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed + -(-self.save_numel(T) * itemsize // 8)
+        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed + -(-self.state_numel(T) * itemsize // 8)
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:

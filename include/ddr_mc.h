@@ -56,6 +56,8 @@ typedef struct {
   int32_t max_block_reaches;  /* cap on reaches per workgroup (0 = auto)             [in]  */
   int32_t target_blocks;      /* desired workgroups (0 = auto: CU count)             [in]  */
   int32_t max_resident;       /* co-resident workgroups of the device (0 = query)    [in]  */
+  int32_t steps_hint;         /* expected timesteps per launch, for load balancing   [in]  */
+                              /* (0 = 8760; any T is correct, this only weighs work)       */
 } ddr_build_opts;
 
 typedef struct {
@@ -135,8 +137,9 @@ enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4 };
  *   qprime     (T, N) lateral inflow, time-major, reference order
  *   q0         (N) carried discharge (DDR_FWD_CARRY) or NULL
  *   runoff     (N, T), or NULL / DDR_FWD_NO_RUNOFF (e.g. gauges: ddr_gauge_reduce afterwards)
- *   x_save     required: the routed states in the schedule layout (save_elems_per_t * T +
- *              save_elems_fixed reals); runoff is emitted from it by a tiled transpose
+ *   x_save     required workspace (save_elems_per_t * T + save_elems_fixed reals): the routed
+ *              states, then q' * flow_scale, both in the schedule layout; runoff is emitted from
+ *              the states by a tiled transpose; keep it unchanged for ddr_mc_backward
  *   bnd        forward boundary buffer (bnd_elems_per_t * T doubles; may be NULL if n_cut == 0);
  *              must be kept unchanged for ddr_mc_backward
  *   status     device status block (status_bytes)
@@ -188,6 +191,20 @@ ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow_host, const
 /* gradA[k] = -gradb[row(k)] * x[col(k)] for CSR (device int64 crow/col). */
 ddr_status ddr_tri_grad_values(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
                                const float* gradb, const float* x, float* grad_values, void* stream);
+
+/* Kernel timing (measurement hook, no reference counterpart).  While enabled, every routing
+ * launch brackets its main kernel (route_forward_kernel / route_backward_kernel) with HIP events
+ * on the launch stream.  ddr_kernel_ms(0 = forward, 1 = backward) synchronises on the last such
+ * pair and returns its duration in milliseconds. */
+ddr_status ddr_set_kernel_timing(int32_t enable);
+ddr_status ddr_kernel_ms(int32_t which, float* ms);
+
+/* Per-workgroup launch profile (debug).  When `buf` is non-null, the next routing launches write
+ * 16 uint64 per workgroup: start and end (s_memrealtime, 100 MHz), time spent waiting on
+ * inter-workgroup imports, the hardware id (HW_ID | XCC_ID << 32), then the time at every 1024th
+ * tick.  `buf` is a zeroed device array of at least 16 * n_blocks uint64; which = 0 (forward) or
+ * 1 (backward). */
+ddr_status ddr_set_block_profile(int32_t which, uint64_t* buf);
 
 /* Device capacity helpers. */
 ddr_status ddr_device_info(int32_t* n_cu, int32_t* max_resident_blocks);

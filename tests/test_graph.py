@@ -117,7 +117,8 @@ def test_partition_invariants(cap):
                 stack.append(w)
     assert seen == len(counts), "block dependency graph has a cycle"
     # save buffer sizes
-    assert g.save_numel(10) == net.n * 10 + g.info.save_elems_fixed
+    assert g.save_numel(10) == 2 * net.n * 10 + g.info.save_elems_fixed
+    assert g.state_numel(10) * 2 == g.save_numel(10)
 
 
 def test_capacity_error_when_too_many_coresident_blocks():
