@@ -36,9 +36,9 @@ constexpr int kChunk = DDR_CHUNK;
 // Parameter-gradient partial sums are flushed to the fp64 accumulators every kGradFlush steps
 // (aligned to the step index, so the summation grouping does not depend on the partition).
 constexpr int kGradFlush = 32;
-// Transpose tiles between the (reach, step) layouts of the API and the tick-major schedule layout.
+// Transpose tiles (reaches) between the (reach, step) layouts of the API and the tick-major
+// schedule layout.
 constexpr int kTileR = 64;
-constexpr int kTileT = 64;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`

@@ -569,13 +569,10 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
 
 // ============================================================================================
 // Layout transposes between the API's (reach, step) arrays and the schedule layout of x_save
-// (per workgroup, tick-major: row tau = t + off(r) holds its nloc reaches contiguously).  One
-// 256-thread workgroup per kTileR x kTileT tile; both sides coalesced through an LDS tile.
+// (per workgroup, tick-major: row tau = t + off(r) holds its nloc reaches contiguously).  Each
+// thread issues all its loads before the first is consumed (memory-level parallelism); the tile's
+// reference ids are staged in LDS so the scattered side has no dependent global loads.
 // ============================================================================================
-// Each thread moves kTileT * kTileR / 256 = 16 elements: all 16 loads are issued before the first
-// is consumed (memory-level parallelism), and the tile's reference ids are staged in LDS so the
-// scattered side has no dependent global loads.
-constexpr int kTrPer = kTileR * kTileT / 256;
 
 // q'[max(t-1, 0), ref] * flow_scale[ref] -> qs[tick(t, r)] (mmc.py:303-304, 421-424): the routing
 // kernels then read one contiguous row per tick instead of scattered 4-byte values of q' rows.
@@ -628,16 +625,25 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   }
 }
 
+// Tiles of kTileR reaches x TrSteps<R> steps, 1024 threads, 16 elements per thread: the (reach,
+// step) side moves whole rows of TrSteps steps per reach (1 KiB), the schedule side runs of
+// positions of one tick offset; the tile (~66 KiB) is staged in LDS.
+template <typename R>
+constexpr int TrSteps = 1024 / sizeof(R);
+constexpr int kTrThreads = 1024;
+
 // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
 template <typename R>
-__global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
-  __shared__ R tile[kTileT][kTileR + 1];
+__global__ void __launch_bounds__(kTrThreads) emit_runoff_kernel(RouteArgs a) {
+  constexpr int TS = TrSteps<R>, PER = kTileR * TS / kTrThreads;
+  constexpr int RS = kTrThreads / kTileR, TSS = kTrThreads / TS;  // row strides of the two phases
+  __shared__ R tile[TS][kTileR + 1];
   __shared__ int sref[kTileR];
   const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
   const BlockDesc B = a.s.blocks[b];
   const int nr = min(kTileR, B.nloc - r0);
   const int64_t T = a.T;
-  const int64_t t0 = (int64_t)blockIdx.y * kTileT;
+  const int64_t t0 = (int64_t)blockIdx.y * TS;
   const R* xs = static_cast<const R*>(a.x_save) + T * B.pos0 + B.pre_dn;
   R* out = static_cast<R*>(a.runoff);
   const R qlb = R(a.c[1]);
@@ -647,22 +653,22 @@ __global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
     const int i = tid % kTileR, j0 = tid / kTileR;  // reach fastest: coalesced along a tick row
     const int ic = i < nr ? i : 0;
     const int off = a.s.off[B.pos0 + r0 + ic];
-    R v[kTrPer];
+    R v[PER];
 #pragma unroll
-    for (int m = 0; m < kTrPer; ++m) {
-      int64_t t = t0 + j0 + 4 * m;
+    for (int m = 0; m < PER; ++m) {
+      int64_t t = t0 + j0 + RS * m;
       t = t < T ? t : T - 1;
       v[m] = xs[(t + off) * B.nloc + r0 + ic];
     }
 #pragma unroll
-    for (int m = 0; m < kTrPer; ++m) tile[j0 + 4 * m][i] = v[m];
+    for (int m = 0; m < PER; ++m) tile[j0 + RS * m][i] = v[m];
   }
   __syncthreads();
-  const int j = tid % kTileT, i0 = tid / kTileT;  // step fastest: coalesced along a reach row
+  const int j = tid % TS, i0 = tid / TS;  // step fastest: coalesced along a reach row
   if (t0 + j < T) {
 #pragma unroll
-    for (int m = 0; m < kTrPer; ++m) {
-      const int i = i0 + 4 * m;
+    for (int m = 0; m < PER; ++m) {
+      const int i = i0 + TSS * m;
       if (i < nr) out[(int64_t)sref[i] * T + t0 + j] = rmax(tile[j][i], qlb);
     }
   }
@@ -671,46 +677,48 @@ __global__ void __launch_bounds__(256) emit_runoff_kernel(RouteArgs a) {
 // gs[tick(t, r)] = dL/drunoff[ref(r), t], or in gauge mode sum over the reach's gauges g of
 // dL/dout[g, t] (mmc.py:405-411: every gauge sums the clamped discharge of its reaches)
 template <typename R>
-__global__ void __launch_bounds__(256) expand_grad_kernel(RouteArgs a) {
-  __shared__ R tile[kTileT][kTileR + 1];
+__global__ void __launch_bounds__(kTrThreads) expand_grad_kernel(RouteArgs a) {
+  constexpr int TS = TrSteps<R>, PER = kTileR * TS / kTrThreads;
+  constexpr int RS = kTrThreads / kTileR, TSS = kTrThreads / TS;
+  __shared__ R tile[TS][kTileR + 1];
   __shared__ int sref[kTileR];
   const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
   const BlockDesc B = a.s.blocks[b];
   const int nr = min(kTileR, B.nloc - r0);
   const int64_t T = a.T;
-  const int64_t t0 = (int64_t)blockIdx.y * kTileT;
+  const int64_t t0 = (int64_t)blockIdx.y * TS;
   const R* go = static_cast<const R*>(a.grad_out);
   R* gs = static_cast<R*>(a.gs) + T * B.pos0 + B.pre_dn;
   const int tid = threadIdx.x;
   if (tid < kTileR) sref[tid] = a.s.ref[B.pos0 + r0 + (tid < nr ? tid : 0)];
   __syncthreads();
   {
-    const int j = tid % kTileT, i0 = tid / kTileT;
+    const int j = tid % TS, i0 = tid / TS;  // step fastest: coalesced along a reach row
     const int64_t tc = t0 + j < T ? t0 + j : T - 1;
-    R v[kTrPer];
+    R v[PER];
     if (a.g_roff) {
 #pragma unroll
-      for (int m = 0; m < kTrPer; ++m) {
-        const int64_t ref = sref[i0 + 4 * m];
+      for (int m = 0; m < PER; ++m) {
+        const int64_t ref = sref[i0 + TSS * m];
         R g = R(0);
         for (int64_t q = a.g_roff[ref]; q < a.g_roff[ref + 1]; ++q) g = g + go[a.g_rg[q] * T + tc];
         v[m] = g;
       }
     } else {
 #pragma unroll
-      for (int m = 0; m < kTrPer; ++m) v[m] = go[(int64_t)sref[i0 + 4 * m] * T + tc];
+      for (int m = 0; m < PER; ++m) v[m] = go[(int64_t)sref[i0 + TSS * m] * T + tc];
     }
 #pragma unroll
-    for (int m = 0; m < kTrPer; ++m) tile[j][i0 + 4 * m] = v[m];
+    for (int m = 0; m < PER; ++m) tile[j][i0 + TSS * m] = v[m];
   }
   __syncthreads();
-  const int i = tid % kTileR, j0 = tid / kTileR;
+  const int i = tid % kTileR, j0 = tid / kTileR;  // reach fastest: coalesced along a tick row
   if (i < nr) {
     const int off = a.s.off[B.pos0 + r0 + i];
 #pragma unroll
-    for (int m = 0; m < kTrPer; ++m) {
-      const int64_t t = t0 + j0 + 4 * m;
-      if (t < T) gs[(t + off) * B.nloc + r0 + i] = tile[j0 + 4 * m][i];
+    for (int m = 0; m < PER; ++m) {
+      const int64_t t = t0 + j0 + RS * m;
+      if (t < T) gs[(t + off) * B.nloc + r0 + i] = tile[j0 + RS * m][i];
     }
   }
 }
@@ -799,8 +807,8 @@ int max_resident_blocks(const Graph* g, bool backward) {
 template <typename R>
 hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream) {
   if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
-  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + kTileT - 1) / kTileT));
-  hipLaunchKernelGGL(emit_runoff_kernel<R>, grid, dim3(256), 0, stream, a);
+  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + TrSteps<R> - 1) / TrSteps<R>));
+  hipLaunchKernelGGL(emit_runoff_kernel<R>, grid, dim3(kTrThreads), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -821,8 +829,8 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
 template <typename R>
 hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream) {
   if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
-  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + kTileT - 1) / kTileT));
-  hipLaunchKernelGGL(expand_grad_kernel<R>, grid, dim3(256), 0, stream, a);
+  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + TrSteps<R> - 1) / TrSteps<R>));
+  hipLaunchKernelGGL(expand_grad_kernel<R>, grid, dim3(kTrThreads), 0, stream, a);
   return hipGetLastError();
 }
 
