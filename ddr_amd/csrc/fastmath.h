@@ -34,6 +34,32 @@ __device__ __forceinline__ void load_math_tables() {
   for (int i = threadIdx.x; i < 2 * kLnTabN + kExpTabN; i += blockDim.x) t[i] = kMathTab[i];
 }
 
+// fp64 constants of ln_tab / exp_tab.  fp64 VALU instructions take no literal operands on gfx950,
+// so each constant occupies a register pair; the routing kernels pin them in VGPRs (pow_consts_vgpr)
+// instead of letting the compiler hoist them into SGPRs, where they displaced the kernel's uniform
+// values into v_writelane / v_readlane spill traffic.
+struct PowK {
+  double ln2hi, ln2lo, l6, l5, l4, l3;  // ln: split ln 2, log1p coefficients -1/6, 1/5, -1/4, 1/3
+  double invl, lhi, llo, e5, e4, e3;    // exp: 128/ln 2, split ln 2 / 128, 1/120, 1/24, 1/6
+};
+__host__ __device__ constexpr PowK pow_consts() {
+  return PowK{6.93147180369123816490e-01, 1.90821492927058770002e-10, -1.0 / 6.0, 0.2, -0.25, 1.0 / 3.0,
+              1.84664965233787316142e+02, 6.93147180369123816490e-01 / 128.0, 1.90821492927058770002e-10 / 128.0,
+              1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0};
+}
+template <typename V>
+__device__ __forceinline__ V in_vgpr(V x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ PowK pow_consts_vgpr() {
+  PowK k = pow_consts();
+  k.ln2hi = in_vgpr(k.ln2hi); k.ln2lo = in_vgpr(k.ln2lo); k.l6 = in_vgpr(k.l6); k.l5 = in_vgpr(k.l5);
+  k.l4 = in_vgpr(k.l4); k.l3 = in_vgpr(k.l3); k.invl = in_vgpr(k.invl); k.lhi = in_vgpr(k.lhi);
+  k.llo = in_vgpr(k.llo); k.e5 = in_vgpr(k.e5); k.e4 = in_vgpr(k.e4); k.e3 = in_vgpr(k.e3);
+  return k;
+}
+
 __device__ __forceinline__ float div_rn(float a, float b) {
   float y = __builtin_amdgcn_rcpf(b);
   const float e = fmaf(-b, y, 1.0f);
@@ -44,34 +70,29 @@ __device__ __forceinline__ float div_rn(float a, float b) {
 }
 
 // ln(x) for fp32 x > 0 normal, fp64 result, absolute error ~1e-16 (table-driven).
-__device__ __forceinline__ double ln_tab(float x) {
-  constexpr double kLn2Hi = 6.93147180369123816490e-01;
-  constexpr double kLn2Lo = 1.90821492927058770002e-10;
+__device__ __forceinline__ double ln_tab(float x, const PowK& K = pow_consts()) {
   const unsigned bits = __float_as_uint(x);
   const int e = (int)(bits >> 23) - 127;
   const unsigned j = (bits >> 16) & 127u;
   const double m = (double)__uint_as_float((bits & 0x7FFFFFu) | 0x3F800000u);  // [1, 2)
   const double2 cl = reinterpret_cast<const double2*>(math_lds())[j];           // (c_j, -ln c_j)
   const double r = fma(m, cl.x, -1.0);                                          // exact
-  double t = fma(r, -1.0 / 6.0, 0.2);
-  t = fma(t, r, -0.25);
-  t = fma(t, r, 1.0 / 3.0);
+  double t = fma(r, K.l6, K.l5);
+  t = fma(t, r, K.l4);
+  t = fma(t, r, K.l3);
   t = fma(t, r, -0.5);
   const double l1p = fma(t, r * r, r);
   const double de = (double)e;
-  return fma(de, kLn2Hi, fma(de, kLn2Lo, cl.y + l1p));
+  return fma(de, K.ln2hi, fma(de, K.ln2lo, cl.y + l1p));
 }
 
 // exp(z) for |z| < 700, fp64, relative error ~2e-16 (table-driven).
-__device__ __forceinline__ double exp_tab(double z) {
-  constexpr double kInvL = 1.84664965233787316142e+02;        // 128 / ln 2
-  constexpr double kLHi = 6.93147180369123816490e-01 / 128.0;  // ln 2 / 128, split (exact products)
-  constexpr double kLLo = 1.90821492927058770002e-10 / 128.0;
-  const double kd = __builtin_rint(z * kInvL);
+__device__ __forceinline__ double exp_tab(double z, const PowK& K = pow_consts()) {
+  const double kd = __builtin_rint(z * K.invl);
   const int k = (int)kd;
-  const double r = fma(-kd, kLLo, fma(-kd, kLHi, z));          // |r| <= ln2 / 256
-  double t = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  t = fma(t, r, 1.0 / 6.0);
+  const double r = fma(-kd, K.llo, fma(-kd, K.lhi, z));                      // |r| <= ln2 / 256
+  double t = fma(r, K.e5, K.e4);
+  t = fma(t, r, K.e3);
   t = fma(t, r, 0.5);
   t = fma(t, r, 1.0);
   t = fma(t, r, 1.0);                                          // exp(r)
@@ -80,10 +101,58 @@ __device__ __forceinline__ double exp_tab(double z) {
 }
 
 // x^y (x > 0) rounded to fp32; ln_out receives ln(x) (fp64) for derivative use.
-__device__ __forceinline__ float pow_pos(float x, float y, double* ln_out = nullptr) {
-  const double l = ln_tab(x);
+__device__ __forceinline__ float pow_pos(float x, float y, double* ln_out = nullptr, const PowK& K = pow_consts()) {
+  const double l = ln_tab(x, K);
   if (ln_out) *ln_out = l;
-  return (float)exp_tab((double)y * l);
+  return (float)exp_tab((double)y * l, K);
+}
+
+// ---- lockstep forms: NP independent evaluations advanced one operation at a time, so a wave
+// carries NP dependency chains at once (the routing ticks are latency-bound at 4 waves/SIMD) ----
+#define DDR_FOR_NP _Pragma("unroll") for (int h = 0; h < NP; ++h)
+
+template <int NP>
+__device__ __forceinline__ void div_rn_np(const float (&a)[NP], const float (&b)[NP], float (&q)[NP]) {
+  float y[NP], e[NP], r[NP];
+  DDR_FOR_NP y[h] = __builtin_amdgcn_rcpf(b[h]);
+  DDR_FOR_NP e[h] = fmaf(-b[h], y[h], 1.0f);
+  DDR_FOR_NP y[h] = fmaf(e[h], y[h], y[h]);
+  DDR_FOR_NP q[h] = a[h] * y[h];
+  DDR_FOR_NP r[h] = fmaf(-q[h], b[h], a[h]);
+  DDR_FOR_NP q[h] = fmaf(r[h], y[h], q[h]);
+}
+
+template <int NP>
+__device__ __forceinline__ void pow_pos_np(const float (&x)[NP], const float (&y)[NP], float (&out)[NP],
+                                           const PowK& K) {
+  const double2* lt = reinterpret_cast<const double2*>(math_lds());
+  const double* et = math_lds() + 2 * kLnTabN;
+  double m[NP], r[NP], t[NP], de[NP], l[NP], z[NP], kd[NP];
+  double2 cl[NP];
+  int k[NP];
+  DDR_FOR_NP {
+    const unsigned bits = __float_as_uint(x[h]);
+    de[h] = (double)((int)(bits >> 23) - 127);
+    cl[h] = lt[(bits >> 16) & 127u];
+    m[h] = (double)__uint_as_float((bits & 0x7FFFFFu) | 0x3F800000u);
+  }
+  DDR_FOR_NP r[h] = fma(m[h], cl[h].x, -1.0);
+  DDR_FOR_NP t[h] = fma(r[h], K.l6, K.l5);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], K.l4);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], K.l3);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], -0.5);
+  DDR_FOR_NP t[h] = fma(t[h], r[h] * r[h], r[h]);
+  DDR_FOR_NP l[h] = fma(de[h], K.ln2hi, fma(de[h], K.ln2lo, cl[h].y + t[h]));
+  DDR_FOR_NP z[h] = (double)y[h] * l[h];
+  DDR_FOR_NP kd[h] = __builtin_rint(z[h] * K.invl);
+  DDR_FOR_NP k[h] = (int)kd[h];
+  DDR_FOR_NP r[h] = fma(-kd[h], K.llo, fma(-kd[h], K.lhi, z[h]));
+  DDR_FOR_NP t[h] = fma(r[h], K.e5, K.e4);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], K.e3);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], 0.5);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], 1.0);
+  DDR_FOR_NP t[h] = fma(t[h], r[h], 1.0);
+  DDR_FOR_NP out[h] = (float)__builtin_amdgcn_ldexp(et[k[h] & 127] * t[h], k[h] >> 7);
 }
 
 }  // namespace ddr

@@ -277,7 +277,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
         mv = std::max(mv, bv[b]);
         mc = std::max(mc, bc[b]);
       }
-      const size_t need = std::max(route_lds_bytes(ms, mv, false, 4), route_lds_bytes(ms, mc, true, 4));
+      const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, false, 4),
+                                   route_lds_bytes(route_slot_stride((int)ms), mc, true, 4));
       if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld lds %zu\n", (long)ms, (long)mv, (long)mc, need);
       if (need > kLdsBudget) {
         if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");

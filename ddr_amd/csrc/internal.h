@@ -41,6 +41,9 @@ constexpr int kGradFlush = 32;
 constexpr int kTileR = 64;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+// LDS slots per buffer of the routing kernels: every block's nloc + nvirt slots, one zero slot
+// (missing upstreams of the forward read it), rounded up to even (16-B aligned statics rows).
+__host__ __device__ inline int route_slot_stride(int max_slots) { return (max_slots + 2) & ~1; }
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
 //   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64

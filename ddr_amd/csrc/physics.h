@@ -21,12 +21,15 @@ namespace ddr {
 template <typename R>
 struct Consts {
   R dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub;
+  PowK pk;  // fp64 constants of the fp32 pow (register-pinned by the routing kernels)
 };
 
 __device__ __forceinline__ float dv(float a, float b) { return div_rn(a, b); }
 __device__ __forceinline__ double dv(double a, double b) { return a / b; }
-__device__ __forceinline__ float pw(float x, float y, double* ln_x = nullptr) { return pow_pos(x, y, ln_x); }
-__device__ __forceinline__ double pw(double x, double y, double* ln_x = nullptr) {
+__device__ __forceinline__ float pw(float x, float y, double* ln_x = nullptr, const PowK& K = pow_consts()) {
+  return pow_pos(x, y, ln_x, K);
+}
+__device__ __forceinline__ double pw(double x, double y, double* ln_x = nullptr, const PowK& = pow_consts()) {
   if (ln_x) *ln_x = log(x);
   return pow(x, y);
 }
@@ -45,17 +48,19 @@ __device__ __forceinline__ float dvf(float a, float b) {
 template <bool Fast>
 __device__ __forceinline__ double dvf(double a, double b) { return a / b; }
 template <bool Fast>
-__device__ __forceinline__ float pwf(float x, float y, double* ln_x = nullptr) {
+__device__ __forceinline__ float pwf(float x, float y, double* ln_x = nullptr, const PowK& K = pow_consts()) {
   if constexpr (Fast) {
     const float l2 = __builtin_amdgcn_logf(x);  // log2 x
     if (ln_x) *ln_x = (double)(l2 * 0.69314718f);
     return __builtin_amdgcn_exp2f(y * l2);
   } else {
-    return pow_pos(x, y, ln_x);
+    return pow_pos(x, y, ln_x, K);
   }
 }
 template <bool Fast>
-__device__ __forceinline__ double pwf(double x, double y, double* ln_x = nullptr) { return pw(x, y, ln_x); }
+__device__ __forceinline__ double pwf(double x, double y, double* ln_x = nullptr, const PowK& = pow_consts()) {
+  return pw(x, y, ln_x);
+}
 template <bool Fast>
 __device__ __forceinline__ float sqf(float a) {
   if constexpr (Fast) return __builtin_amdgcn_sqrtf(a);
@@ -68,6 +73,12 @@ template <typename R>
 __device__ __forceinline__ R rmax(R a, R b) { return a > b ? a : b; }  // torch.clamp(min=) on finite
 template <typename R>
 __device__ __forceinline__ R rmin(R a, R b) { return a < b ? a : b; }
+template <typename R>
+__device__ __forceinline__ R rclamp(R x, R lo, R hi) { return rmin(rmax(x, lo), hi); }
+// fp32: one v_med3_f32 each (equal to torch.clamp for the finite values of the physics)
+__device__ __forceinline__ float rmax(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); }
+__device__ __forceinline__ float rmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
+__device__ __forceinline__ float rclamp(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 
 // torch: pow(R, 2 / 3) -- the Python double 2/3 is rounded to the tensor dtype.
 template <typename R>
@@ -127,21 +138,21 @@ __device__ __forceinline__ void coefficients(const ReachStatic<R>& s, R Q, const
   double ln_ratio = 0.0, ln_depth = 0.0;
   const R num = (Q * s.n) * s.qe1();
   const R ratio = dvf<Fast>(num, s.dd);
-  const R pwv = pwf<Fast>(ratio, s.expo, gk ? &ln_ratio : nullptr);
+  const R pwv = pwf<Fast>(ratio, s.expo, gk ? &ln_ratio : nullptr, c.pk);
   const R depth = rmax(pwv, c.dlb);
-  const R dq = pwf<Fast>(depth, s.qe, gk ? &ln_depth : nullptr);
+  const R dq = pwf<Fast>(depth, s.qe, gk ? &ln_depth : nullptr, c.pk);
   const R tw = s.p * dq;
   const R ssr = dvf<Fast>(tw * s.qe, R(2) * depth);
-  const R ss = rmin(rmax(ssr, c.sslb), c.ssub);
+  const R ss = rclamp(ssr, c.sslb, c.ssub);
   const R bwr = tw - (R(2) * ss) * depth;
   const R bw = rmax(bwr, c.bwlb);
   const R area = ((tw + bw) * depth) * R(0.5);  // x / 2 == x * 0.5 exactly
   const R sq = sqf<Fast>(R(1) + ss * ss);
   const R wp = bw + (R(2) * depth) * sq;
   const R Rh = dvf<Fast>(area, wp);
-  const R r23 = pwf<Fast>(Rh, two_thirds<R>());
+  const R r23 = pwf<Fast>(Rh, two_thirds<R>(), nullptr, c.pk);
   const R v = (s.inv_n * r23) * s.sqrtS;
-  const R vc = rmin(rmax(v, c.vlb), c.vub);
+  const R vc = rclamp(v, c.vlb, c.vub);
   const R cel = dvf<Fast>(vc * R(5), R(3));
   const R k = dvf<Fast>(s.L, cel);
   const R twok = R(2) * k;
@@ -159,6 +170,74 @@ __device__ __forceinline__ void coefficients(const ReachStatic<R>& s, R Q, const
     gk->r23 = r23; gk->v = v; gk->cel = cel; gk->twok = twok; gk->den = den;
     gk->ln_ratio = R(ln_ratio); gk->ln_depth = R(ln_depth);
   }
+}
+
+// Lockstep form of coefficients<R> (forward, exact operation set) for NP reaches: every operation
+// is issued for all NP reaches before the next, so a wave runs NP independent chains.
+template <typename R>
+struct PhysOut {
+  R c1, c2, c3, c4, tw, ss;
+};
+template <int NP>
+__device__ __forceinline__ void dv_np(const float (&a)[NP], const float (&b)[NP], float (&q)[NP]) { div_rn_np<NP>(a, b, q); }
+template <int NP>
+__device__ __forceinline__ void dv_np(const double (&a)[NP], const double (&b)[NP], double (&q)[NP]) {
+  DDR_FOR_NP q[h] = a[h] / b[h];
+}
+template <int NP>
+__device__ __forceinline__ void pw_np(const float (&x)[NP], const float (&y)[NP], float (&o)[NP], const PowK& K) {
+  pow_pos_np<NP>(x, y, o, K);
+}
+template <int NP>
+__device__ __forceinline__ void pw_np(const double (&x)[NP], const double (&y)[NP], double (&o)[NP], const PowK&) {
+  DDR_FOR_NP o[h] = pow(x[h], y[h]);
+}
+
+template <typename R, int NP>
+__device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], const R (&Q)[NP], const Consts<R>& c,
+                                                PhysOut<R> (&o)[NP]) {
+  R a[NP], b[NP], ratio[NP], depth[NP], dq[NP], e[NP], ssr[NP], ss[NP], bw[NP], area[NP], wp[NP], Rh[NP],
+      r23[NP], twok[NP], den[NP];
+  DDR_FOR_NP a[h] = (Q[h] * s[h].n) * s[h].qe1();
+  DDR_FOR_NP b[h] = s[h].dd;
+  dv_np<NP>(a, b, ratio);
+  DDR_FOR_NP e[h] = s[h].expo;
+  pw_np<NP>(ratio, e, depth, c.pk);
+  DDR_FOR_NP depth[h] = rmax(depth[h], c.dlb);
+  DDR_FOR_NP e[h] = s[h].qe;
+  pw_np<NP>(depth, e, dq, c.pk);
+  DDR_FOR_NP o[h].tw = s[h].p * dq[h];
+  DDR_FOR_NP a[h] = o[h].tw * s[h].qe;
+  DDR_FOR_NP b[h] = R(2) * depth[h];
+  dv_np<NP>(a, b, ssr);
+  DDR_FOR_NP ss[h] = rclamp(ssr[h], c.sslb, c.ssub);
+  DDR_FOR_NP o[h].ss = ss[h];
+  DDR_FOR_NP bw[h] = rmax(o[h].tw - (R(2) * ss[h]) * depth[h], c.bwlb);
+  DDR_FOR_NP area[h] = ((o[h].tw + bw[h]) * depth[h]) * R(0.5);
+  DDR_FOR_NP a[h] = rsqrt_(R(1) + ss[h] * ss[h]);
+  DDR_FOR_NP wp[h] = bw[h] + (R(2) * depth[h]) * a[h];
+  dv_np<NP>(area, wp, Rh);
+  DDR_FOR_NP e[h] = two_thirds<R>();
+  pw_np<NP>(Rh, e, r23, c.pk);
+  DDR_FOR_NP a[h] = rclamp((s[h].inv_n * r23[h]) * s[h].sqrtS, c.vlb, c.vub) * R(5);
+  DDR_FOR_NP b[h] = R(3);
+  dv_np<NP>(a, b, e);                                  // celerity
+  DDR_FOR_NP a[h] = s[h].L;
+  dv_np<NP>(a, e, b);                                  // k = L / c
+  DDR_FOR_NP twok[h] = R(2) * b[h];
+  DDR_FOR_NP den[h] = (twok[h] * s[h].omX()) + c.dt;
+  DDR_FOR_NP a[h] = c.dt - twok[h] * s[h].X;
+  dv_np<NP>(a, den, b);
+  DDR_FOR_NP o[h].c1 = b[h];
+  DDR_FOR_NP a[h] = c.dt + twok[h] * s[h].X;
+  dv_np<NP>(a, den, b);
+  DDR_FOR_NP o[h].c2 = b[h];
+  DDR_FOR_NP a[h] = (twok[h] * s[h].omX()) - c.dt;
+  dv_np<NP>(a, den, b);
+  DDR_FOR_NP o[h].c3 = b[h];
+  DDR_FOR_NP a[h] = R(2) * c.dt;
+  dv_np<NP>(a, den, b);
+  DDR_FOR_NP o[h].c4 = b[h];
 }
 
 // VJP of (c1, c2, c3, c4) w.r.t. (Q, n, q_spatial, p_spatial) at the point described by g.

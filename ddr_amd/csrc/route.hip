@@ -19,6 +19,8 @@
 // Reference semantics (file:line in /root/reference):
 //   forward  src/ddr/routing/mmc.py:365-443, 487-559, 25-66; routing/utils.py:587-600 (fp64 solve)
 //   backward routing/utils.py:629-692 + torch autograd of mmc.py/trapezoidal.py (hand adjoint)
+#include <type_traits>
+
 #include "internal.h"
 #include "physics.h"
 #include "route_args.h"
@@ -66,11 +68,15 @@ template <typename R>
 __device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a);
 template <>
 __device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a) {
-  return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7]};
+#ifndef DDR_PIN_POWK
+#define DDR_PIN_POWK 1
+#endif
+  return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7],
+                       DDR_PIN_POWK ? pow_consts_vgpr() : pow_consts()};
 }
 template <>
 __device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a) {
-  return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7]};
+  return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7], pow_consts()};
 }
 
 template <typename R>
@@ -84,11 +90,12 @@ __device__ __forceinline__ ReachStatic<R> load_static(const RouteArgs& a, int re
   return make_static<R>(n[ref], q[ref], p[(int64_t)ref * a.p_stride], S[ref], L[ref], X[ref]);
 }
 
-// Packed upstream descriptor: u0 (13 bits) | u1 (13 bits) << 13 | min(nup, 15) << 26.
-__device__ __forceinline__ unsigned pack_up(const RouteArgs& a, int P) {
+// Packed upstream descriptor: u0 (13 bits) | u1 (13 bits) << 13 | min(nup, 15) << 26; a missing
+// upstream reads slot `none` (the forward's zero slot).
+__device__ __forceinline__ unsigned pack_up(const RouteArgs& a, int P, unsigned none = 0u) {
   const int b = a.s.upb[P], c = a.s.upc[P];
-  const unsigned u0 = c > 0 ? (unsigned)a.s.uplist[b] : 0u;
-  const unsigned u1 = c > 1 ? (unsigned)a.s.uplist[b + 1] : 0u;
+  const unsigned u0 = c > 0 ? (unsigned)a.s.uplist[b] : none;
+  const unsigned u1 = c > 1 ? (unsigned)a.s.uplist[b + 1] : none;
   return u0 | (u1 << 13) | ((unsigned)(c < 15 ? c : 15) << 26);
 }
 // Make a per-reach value opaque inside the tick loop so the compiler recomputes what it derives
@@ -125,24 +132,42 @@ __device__ __forceinline__ void prof_end(unsigned long long* p, unsigned long lo
 
 }  // namespace
 
-// Per-reach statics in LDS: six arrays of S reals (n, qe, p, sqrtS, L, X).  The derived fields
-// (dd, expo, 1/n) are recomputed on every read (derive_static): 3 LDS reads and two divisions per
-// reach-step are cheaper than the ~9 registers per reach that holding them would cost.
+// Per-reach statics in LDS, interleaved [slot][6] (n, qe, p, sqrtS, L, X): one get is three
+// 2-element LDS reads at immediate offsets (lane stride 24 B: conflict-free).  The derived fields
+// (dd, expo, 1/n) are recomputed on read (derive_static), or taken from registers (get_pre).
 template <typename R>
 struct StatTab {
   R* s;
-  int S;
+  using V2 = typename std::conditional<sizeof(R) == 4, float2, double2>::type;
   __device__ __forceinline__ void put(int r, const ReachStatic<R>& v) const {
-    s[r] = v.n;
-    s[S + r] = v.qe;
-    s[2 * S + r] = v.p;
-    s[3 * S + r] = v.sqrtS;
-    s[4 * S + r] = v.L;
-    s[5 * S + r] = v.X;
+    R* q = s + 6 * r;
+    q[0] = v.n;
+    q[1] = v.qe;
+    q[2] = v.p;
+    q[3] = v.sqrtS;
+    q[4] = v.L;
+    q[5] = v.X;
   }
   template <bool Fast = false>
   __device__ __forceinline__ ReachStatic<R> get(int r) const {
-    return derive_static<R, Fast>(s[r], s[S + r], s[2 * S + r], s[3 * S + r], s[4 * S + r], s[5 * S + r]);
+    const V2* q = reinterpret_cast<const V2*>(s + 6 * r);
+    const V2 a = q[0], b = q[1], c = q[2];
+    return derive_static<R, Fast>(a.x, a.y, b.x, b.y, c.x, c.y);
+  }
+  __device__ __forceinline__ ReachStatic<R> get_pre(int r, R expo, R inv_n) const {
+    const V2* q = reinterpret_cast<const V2*>(s + 6 * r);
+    const V2 a = q[0], b = q[1], c = q[2];
+    ReachStatic<R> v;
+    v.n = a.x;
+    v.qe = a.y;
+    v.p = b.x;
+    v.sqrtS = b.y;
+    v.dd = (b.x * b.y) + R(1e-8);
+    v.expo = expo;
+    v.inv_n = inv_n;
+    v.L = c.x;
+    v.X = c.y;
+    return v;
   }
 };
 
@@ -158,6 +183,10 @@ struct StatTab {
 template <typename R, int KR>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
+#ifndef DDR_FWD_NP
+#define DDR_FWD_NP 1
+#endif
+  constexpr int NP = KR < DDR_FWD_NP ? KR : DDR_FWD_NP;  // slices whose physics runs in lockstep
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int tid = threadIdx.x;
   // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
@@ -166,7 +195,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int S = a.slot_stride;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
-  const StatTab<R> tab{reinterpret_cast<R*>(sx + S), S};                // [6][S]
+  const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
@@ -179,7 +208,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   int ref[KR], off[KR];
   unsigned up[KR];
   bool cut[KR];
-  R Q[KR], In[KR], qa[KR], qb[KR];
+  R Q[KR], In[KR], qa[KR], qb[KR], ex[KR], inv[KR];  // ex, inv: the static divisions, kept in registers
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -187,12 +216,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
-    up[k] = pack_up(a, P);
+    up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
     cut[k] = a.s.cut[P] >= 0;
     Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
-    if (hk) tab.put(r, load_static<R>(a, ref[k]));
+    const ReachStatic<R> st = load_static<R>(a, ref[k]);
+    ex[k] = st.expo;
+    inv[k] = st.inv_n;
+    if (hk) tab.put(r, st);
   }
+  if (tid == 0) sx[S - 1] = 0.0;
   const bool vown = tid < B.nvirt;
   int v_off = 0;
   if (vown) v_off = a.s.v_off[B.virt0 + tid];
@@ -223,6 +256,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       ref[k] = opq(ref[k]);
       off[k] = opq(off[k]);
       up[k] = opq(up[k]);
+      ex[k] = opq(ex[k]);
+      inv[k] = opq(inv[k]);
     }
     if (B.nvirt > 0 && (tau % kChunk) == 0) {
       // import the next chunk of every virtual inflow (x of the upstream block's reach)
@@ -239,67 +274,80 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     prefetch(tau + 1, qnext, tq);
+    R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
-    // ---- compute: one reach at a time (gather, physics, fp64 column sweep) -------------------
+    // ---- compute, NP slices at a time: their physics in lockstep (NP independent dependency
+    //      chains per wave: the tick is latency-bound at 4 waves per SIMD), then per slice the
+    //      fp64 column sweep and the stores -------------------------------------------------------
 #pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      if (wbase + k * BS >= B.nloc) continue;
-      const int r = tq + k * BS;
-      const bool hk = r < B.nloc;
-      const int t = tau - off[k];
-      const int nup = up_n(up[k]);
-      const ReachStatic<R> st = tab.get(hk ? r : 0);
-      const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
-      R c1, c2, c3, c4, tw, ss;
-      coefficients<R>(st, Q[k], cs, c1, c2, c3, c4, tw, ss);
-      const R qc = rmax(qv, cs.qlb);                                  // mmc.py:421-424
-      const R b = ((c2 * In[k]) + (c3 * Q[k])) + (c4 * qc);           // mmc.py:535-538
-      const double x0v = sx[up_0(up[k])];
-      const double x1v = sx[up_1(up[k])];
-      // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
-      const bool raw = (t == 0 && carry);
-      auto qf = [&](double x) -> R {
-        const R xr = R(x);
-        return raw ? xr : rmax(xr, cs.qlb);
-      };
-      const double dc1 = (double)c1;
-      double acc = (double)b;                                         // utils.py:587-600 (fp64)
-      acc = acc + (nup > 0 ? dc1 * x0v : 0.0);
-      acc = acc + (nup > 1 ? dc1 * x1v : 0.0);
-      double hot = (double)qv;                                        // mmc.py:25-66 (hot start)
-      hot = hot + (nup > 0 ? x0v : 0.0);
-      hot = hot + (nup > 1 ? x1v : 0.0);
-      R inn = R(0);                                                   // I(t+1) = N @ Q_t, ascending columns
-      inn = inn + (nup > 0 ? qf(x0v) : R(0));
-      inn = inn + (nup > 1 ? qf(x1v) : R(0));
-      if (nup > 2) {
-        const int P = B.pos0 + r;
-        const int bb = a.s.upb[P], c = a.s.upc[P];
-        for (int j = 2; j < c; ++j) {
-          const double xj = sx[a.s.uplist[bb + j]];
-          acc = acc + dc1 * xj;
-          hot = hot + xj;
-          inn = inn + qf(xj);
-        }
+    for (int k0 = 0; k0 < KR; k0 += NP) {
+      if (wbase + k0 * BS >= B.nloc) continue;
+      ReachStatic<R> st[NP];
+      R Qv[NP];
+      PhysOut<R> ph[NP];
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {
+        const int r = tq + (k0 + h) * BS;
+        st[h] = tab.get_pre(r < B.nloc ? r : 0, ex[k0 + h], inv[k0 + h]);
+        Qv[h] = Q[k0 + h];
       }
-      const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
-      xk[k] = x;
-      if (hk && t >= 0 && t < T) {
-        const R xr = R(x);
-        const R Qn = raw ? xr : rmax(xr, cs.qlb);
-        xsave[xs_base + (int64_t)tau * B.nloc + r] = xr;  // runoff is emitted from here (emit_runoff_kernel)
-        if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
-        if (t == T - 1) {
-          if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
-          if (t > 0) {
-            if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = tw;
-            if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ss;
+      coefficients_np<R, NP>(st, Qv, cs, ph);
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {
+        const int k = k0 + h;
+        const int r = tq + k * BS;
+        const bool hk = r < B.nloc;
+        const int t = tau - off[k];
+        const int nup = up_n(up[k]);
+        const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
+        const R qc = rmax(qv, cs.qlb);                                        // mmc.py:421-424
+        const R b = ((ph[h].c2 * In[k]) + (ph[h].c3 * Q[k])) + (ph[h].c4 * qc);  // mmc.py:535-538
+        const double x0v = sx[up_0(up[k])];
+        const double x1v = sx[up_1(up[k])];
+        // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
+        const bool raw = (t == 0 && carry);
+        auto qf = [&](double x) -> R {
+          const R xr = R(x);
+          return raw ? xr : rmax(xr, cs.qlb);
+        };
+        const double dc1 = (double)ph[h].c1;
+        double acc = (double)b;                                         // utils.py:587-600 (fp64)
+        acc = acc + dc1 * x0v;                                          // (+ 0 for a missing upstream)
+        acc = acc + dc1 * x1v;
+        double hot = (double)qv;                                        // mmc.py:25-66 (hot start)
+        hot = hot + x0v;
+        hot = hot + x1v;
+        R inn = R(0);                                                   // I(t+1) = N @ Q_t, ascending columns
+        inn = inn + (nup > 0 ? qf(x0v) : R(0));
+        inn = inn + (nup > 1 ? qf(x1v) : R(0));
+        if (nup > 2) {
+          const int P = B.pos0 + r;
+          const int bb = a.s.upb[P], c = a.s.upc[P];
+          for (int j = 2; j < c; ++j) {
+            const double xj = sx[a.s.uplist[bb + j]];
+            acc = acc + dc1 * xj;
+            hot = hot + xj;
+            inn = inn + qf(xj);
           }
         }
-        Q[k] = Qn;
-        In[k] = inn;
+        const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
+        xk[k] = x;
+        if (hk && t >= 0 && t < T) {
+          const R xr = R(x);
+          const R Qn = raw ? xr : rmax(xr, cs.qlb);
+          xrow[r] = xr;  // runoff is emitted from here (emit_runoff_kernel)
+          if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
+          if (t == T - 1) {
+            if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
+            if (t > 0) {
+              if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = ph[h].tw;
+              if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ph[h].ss;
+            }
+          }
+          Q[k] = Qn;
+          In[k] = inn;
+        }
       }
-      // one reach's chain in flight keeps the register budget of 4 waves per SIMD
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
@@ -351,7 +399,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sa = reinterpret_cast<double*>(smem + kMathTabBytes);  // [S] c1_i * gb_i  (fp64, transposed solve)
   R* sb = reinterpret_cast<R*>(sa + S);                           // [S] c2_i * gb_i
-  const StatTab<R> tab{sb + S, S};                                // [6][S]
+  const StatTab<R> tab{sb + S};                                   // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
@@ -750,13 +798,13 @@ __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
 // ============================================================================================
 template <typename R>
 size_t route_smem_bytes(const Graph* g, bool backward) {
-  return route_lds_bytes((size_t)g->max_slots, (size_t)(backward ? g->max_cout : g->max_virt), backward, sizeof(R));
+  return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)(backward ? g->max_cout : g->max_virt), backward, sizeof(R));
 }
 
 template <typename R, int KR>
 hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream_t stream) {
   const size_t smem = route_smem_bytes<R>(g, backward);
-  a.slot_stride = g->max_slots;
+  a.slot_stride = route_slot_stride(g->max_slots);
   a.ring_stride = backward ? 2 * kChunk : kChunk;
   a.n_cut = g->n_cut;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
