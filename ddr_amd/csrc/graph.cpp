@@ -193,25 +193,42 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     int64_t ncut = 0;
     for (auto& P : pieces) ncut += (g->down[P.root] >= 0);
     // Packing: pieces of equal height share blocks (so the block dependency graph is a DAG),
-    // worst-fit by weight.  A block on a long inter-block chain starts late (forward: blocks near
-    // the outlet wait for the chain above them; backward: blocks near the sources) and runs
-    // T + lag ticks, so pieces are weighted by (T + lag + dmax) / T of the block they landed in and
-    // the packing is repeated: long-chain blocks get fewer reaches and tick faster.
-    std::vector<double> w(pieces.size()), F;
-    for (size_t p = 0; p < pieces.size(); ++p) w[p] = (double)pieces[p].size;
-    std::vector<int64_t> order(pieces.size()), block_of_piece(pieces.size()), load, bdm;
-    std::vector<double> wload;
-    for (int it = 0; it < 3; ++it) {
-      double wsum = 0.0;
-      for (double x : w) wsum += x;
-      const double capw = (double)cap * wsum / (double)n;  // the unweighted cap, scaled by the mean weight
-      std::iota(order.begin(), order.end(), 0);
-      std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-        if (pieces[a].height != pieces[b].height) return pieces[a].height < pieces[b].height;
-        return w[a] > w[b];
-      });
+    // worst-fit by weight.  The blocks of a split basin progress at the pace of their slowest
+    // member (a consumer waits for its producers, forward and backward alike), so every block
+    // holding a piece of a long path needs T + (path length) ticks, not T + dmax: a piece is
+    // weighted by (T + L) / T with L the longest source-to-outlet path through its root, plus one
+    // chunk per inter-block hop on it.  Chain blocks get fewer reaches and tick faster (a tick
+    // costs in proportion to the reaches of a workgroup).
+    std::vector<int64_t> hops_down(pieces.size(), 0);
+    for (size_t p = 0; p < pieces.size(); ++p) {  // parents before children (creation order)
+      const int64_t d = g->down[pieces[p].root];
+      if (d >= 0) hops_down[p] = hops_down[piece[d]] + 1;
+    }
+    std::vector<double> fac(pieces.size());
+    double wsum = 0.0;
+    for (size_t p = 0; p < pieces.size(); ++p) {
+      const int64_t r = pieces[p].root;
+      const double L = (double)(ht[r] + g->dist[r] + kChunk * (hops_down[p] + pieces[p].height));
+      fac[p] = (steps + L) / steps;
+      wsum += (double)pieces[p].size * fac[p];
+    }
+    // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
+    // Pieces are taken by factor (descending) so blocks gather pieces of similar factor; capw is
+    // the smallest (1 % steps) that packs into the target number of workgroups.
+    std::vector<int64_t> order(pieces.size()), block_of_piece(pieces.size()), load;
+    std::vector<double> bcap;
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      if (pieces[a].height != pieces[b].height) return pieces[a].height < pieces[b].height;
+      if (fac[a] != fac[b]) return fac[a] > fac[b];
+      return pieces[a].size > pieces[b].size;
+    });
+    int64_t ncut0 = 0;
+    for (auto& P : pieces) ncut0 += (g->down[P.root] >= 0);
+    const int64_t limit = ncut0 > 0 ? std::min<int64_t>(target, resident) : target;
+    for (double capw = wsum / (double)limit;; capw *= 1.01) {
       load.clear();
-      wload.clear();
+      bcap.clear();
       size_t hstart = 0;  // first block of the current height class
       int64_t curh = -1;
       for (int64_t p : order) {
@@ -221,42 +238,16 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
         }
         int64_t best = -1;
         for (size_t b = hstart; b < load.size(); ++b)
-          if (wload[b] + w[p] <= capw * 1.0001 && load[b] + pieces[p].size <= hard_cap &&
-              (best < 0 || wload[b] < wload[best]))
-            best = (int64_t)b;
+          if ((double)(load[b] + pieces[p].size) <= bcap[b] && (best < 0 || load[b] < load[best])) best = (int64_t)b;
         if (best < 0) {
           best = (int64_t)load.size();
           load.push_back(0);
-          wload.push_back(0.0);
+          bcap.push_back(std::min<double>((double)hard_cap, std::max<double>((double)pieces[p].size, capw / fac[p])));
         }
         load[best] += pieces[p].size;
-        wload[best] += w[p];
         block_of_piece[p] = best;
       }
-      // block lags (ticks) along the block DAG, per cut edge p -> c:
-      //   forward  lagf(c) >= lagf(p) + dmax(p) - dmax(c) + dist_in_piece(d) + 1 + kChunk
-      //   backward lagb(p) >= lagb(c) + dist_in_piece(d) + kChunk
-      const size_t nb = load.size();
-      bdm.assign(nb, 0);
-      for (size_t p = 0; p < pieces.size(); ++p) bdm[block_of_piece[p]] = std::max(bdm[block_of_piece[p]], pieces[p].dmax);
-      std::vector<int64_t> lagf(nb, 0), lagb(nb, 0);
-      for (int sweep = 0; sweep < 1000; ++sweep) {
-        bool changed = false;
-        for (size_t p = 0; p < pieces.size(); ++p) {
-          const int64_t d = g->down[pieces[p].root];
-          if (d < 0) continue;
-          const int64_t pb = block_of_piece[p], cb = block_of_piece[piece[d]];
-          const int64_t lf = lagf[pb] + bdm[pb] - bdm[cb] + dloc_piece[d] + 1 + kChunk;
-          if (lf > lagf[cb]) { lagf[cb] = lf; changed = true; }
-          const int64_t lb = lagb[cb] + dloc_piece[d] + kChunk;
-          if (lb > lagb[pb]) { lagb[pb] = lb; changed = true; }
-        }
-        if (!changed) break;
-      }
-      F.assign(nb, 1.0);
-      for (size_t b = 0; b < nb; ++b)
-        F[b] = (steps + (double)std::max(lagf[b], lagb[b]) + (double)bdm[b]) / steps;
-      for (size_t p = 0; p < pieces.size(); ++p) w[p] = (double)pieces[p].size * F[block_of_piece[p]];
+      if ((int64_t)load.size() <= limit || capw / 1.3 > (double)hard_cap) break;
     }
     const int64_t nblocks = (int64_t)load.size();
     if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part] cap %ld hard %ld pieces %zu blocks %ld cut %ld\n", (long)cap, (long)hard_cap, pieces.size(), (long)nblocks, (long)ncut);
