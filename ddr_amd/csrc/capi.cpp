@@ -121,7 +121,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   RouteArgs a;
   fill_common<R>(a, g, c, r, T, qprime, flags);
   a.q0 = q0;
-  a.runoff = runoff;
+  a.runoff = (flags & DDR_FWD_NO_RUNOFF) ? nullptr : runoff;
   a.x_save = x_save;
   a.bnd = bnd;
   a.status = static_cast<unsigned*>(status);
@@ -134,7 +134,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   DDR_HIP(timing_mark(0, 0, s));
   DDR_HIP(launch_route<R>(g, a, false, s));
   DDR_HIP(timing_mark(0, 1, s));
-  if (runoff && !(flags & DDR_FWD_NO_RUNOFF)) DDR_HIP(launch_emit_runoff<R>(g, a, s));
+  // runoff (N, T) is written by the routing kernel itself (16-B row segments every 4 steps)
   return DDR_OK;
 }
 

@@ -107,6 +107,13 @@ __device__ __forceinline__ V opq(V x) {
   return x;
 }
 __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
+__device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void store4(double* p, double a, double b, double c, double d) {
+  reinterpret_cast<double2*>(p)[0] = make_double2(a, b);
+  reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
+}
 __device__ __forceinline__ int up_0(unsigned u) { return (int)(u & 8191u); }
 __device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u); }
 
@@ -209,6 +216,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   unsigned up[KR];
   bool cut[KR];
   R Q[KR], In[KR], qa[KR], qb[KR], ex[KR], inv[KR];  // ex, inv: the static divisions, kept in registers
+  // runoff (N, T) written from here: the last four steps of each reach, stored 16 B at a time
+  R ob0[KR], ob1[KR], ob2[KR], ob3[KR];
+  R* runoff = static_cast<R*>(a.runoff);
+  const bool emit = runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
+  const bool emit4 = (T & 3) == 0;  // rows 16-B aligned: vector stores
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -220,6 +232,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     cut[k] = a.s.cut[P] >= 0;
     Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
+    ob0[k] = ob1[k] = ob2[k] = ob3[k] = R(0);
     const ReachStatic<R> st = load_static<R>(a, ref[k]);
     ex[k] = st.expo;
     inv[k] = st.inv_n;
@@ -335,7 +348,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if (hk && t >= 0 && t < T) {
           const R xr = R(x);
           const R Qn = raw ? xr : rmax(xr, cs.qlb);
-          xrow[r] = xr;  // runoff is emitted from here (emit_runoff_kernel)
+          xrow[r] = xr;  // the routing state for the adjoint
+          if (emit) {
+            // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
+            ob0[k] = ob1[k];
+            ob1[k] = ob2[k];
+            ob2[k] = ob3[k];
+            ob3[k] = rmax(xr, cs.qlb);
+            R* orow = runoff + (int64_t)ref[k] * T;
+            if (!emit4) orow[t] = ob3[k];
+            else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
+          }
           if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
           if (t == T - 1) {
             if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
