@@ -303,4 +303,99 @@ __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, c
   gp = g_p;
 }
 
+// ---- fp32 adjoint step (backward kernel, fp32 build): the step's physics recomputed in hardware
+// fp32 math and its VJP, folded algebraically.  Equivalent in exact arithmetic to
+// coefficients<float, true> + coefficients_vjp<float, true>; per reach-step ~15 transcendental and
+// ~90 other instructions.  Uses x(t) = c1 Sx + c2 I + c3 Q + c4 qc (the forward solve) to collapse
+// sum_k gc_k c_k into gb x.
+struct AdjOut {
+  float c1, c2, c3, gQ, gn, gq, gp;
+};
+__device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s, float Q, const Consts<float>& c,
+                                                    float gb, float x, float Sx, float I) {
+  constexpr float kLn2 = 0.69314718055994530942f;
+  const float qe = s.qe, qe1 = qe + 1.0f, expo = s.expo;
+  // ---- recompute (geometry/trapezoidal.py:62-97, routing/mmc.py:165-167, 479-484) ----
+  const float num = (Q * s.n) * qe1;
+  const float rdd = __builtin_amdgcn_rcpf(s.dd);
+  const float ratio = num * rdd;
+  const float l2r = __builtin_amdgcn_logf(ratio);
+  const float pw = __builtin_amdgcn_exp2f(expo * l2r);
+  const float depth = rmax(pw, c.dlb);
+  const float l2d = __builtin_amdgcn_logf(depth);
+  const float dq = __builtin_amdgcn_exp2f(qe * l2d);
+  const float tw = s.p * dq;
+  const float td = depth + depth;
+  const float rtd = __builtin_amdgcn_rcpf(td);
+  const float ssr = (tw * qe) * rtd;
+  const float ss = rclamp(ssr, c.sslb, c.ssub);
+  const float bwr = tw - (ss + ss) * depth;
+  const float bw = rmax(bwr, c.bwlb);
+  const float area = ((tw + bw) * depth) * 0.5f;
+  const float u = fmaf(ss, ss, 1.0f);
+  const float isq = __builtin_amdgcn_rsqf(u);
+  const float sq = u * isq;
+  const float wp = fmaf(td, sq, bw);
+  const float rwp = __builtin_amdgcn_rcpf(wp);
+  const float Rh = area * rwp;
+  const float r23 = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(Rh) * (2.0f / 3.0f));
+  const float v = (s.inv_n * r23) * s.sqrtS;
+  const float cel = rclamp(v, c.vlb, c.vub) * (5.0f / 3.0f);
+  const float rcel = __builtin_amdgcn_rcpf(cel);
+  const float twok = 2.0f * (s.L * rcel);
+  const float omX = 1.0f - s.X;
+  const float den = fmaf(twok, omX, c.dt);
+  const float rden = __builtin_amdgcn_rcpf(den);
+  const float tX = twok * s.X;
+  AdjOut o;
+  o.c1 = (c.dt - tX) * rden;
+  o.c2 = (c.dt + tX) * rden;
+  const float c4 = (2.0f * c.dt) * rden;
+  o.c3 = 1.0f - c4;
+  // ---- VJP: gc = gb (Sx, I, Q, qc); sum_k gc_k c_k = gb x ----
+  const float g_twok = gb * fmaf(s.X, I - Sx, omX * (Q - x)) * rden;
+  const float g_cel = -(g_twok * twok) * rcel;                    // k = L / cel
+  const bool vin = (v >= c.vlb) && (v <= c.vub);
+  const float gvv = vin ? (g_cel * (5.0f / 3.0f)) * v : 0.0f;     // dL/d ln v
+  float g_n = -gvv * s.inv_n;
+  const float G = gvv * (2.0f / 3.0f);                            // dL/d ln Rh
+  const float g_area = G * __builtin_amdgcn_rcpf(area);
+  const float g_wp = -G * rwp;
+  // wp = bw + 2 depth sq ; area = (tw + bw) depth / 2
+  const float ha = (g_area * depth) * 0.5f;
+  float g_bw = g_wp + ha;
+  float g_tw = ha;
+  float g_depth = fmaf(2.0f * sq, g_wp, (G + G) * rtd);             // + G / depth
+  float g_ss = ((td * g_wp) * ss) * isq;
+  // bw = max(tw - 2 ss depth, bw_lb)
+  const float g_bwr = (bwr >= c.bwlb) ? g_bw : 0.0f;
+  g_tw += g_bwr;
+  g_ss = fmaf(-td, g_bwr, g_ss);
+  g_depth = fmaf(-(ss + ss), g_bwr, g_depth);
+  // ss = clamp(tw qe / (2 depth))
+  const float g_ssr = (ssr >= c.sslb && ssr <= c.ssub) ? g_ss : 0.0f;
+  const float gsr = g_ssr * rtd;
+  g_tw = fmaf(gsr, qe, g_tw);
+  float g_qe = gsr * tw;
+  g_depth = fmaf(-(g_ssr + g_ssr) * ssr, rtd, g_depth);
+  // tw = p depth^qe
+  float g_p = g_tw * dq;
+  const float gtt = g_tw * tw;
+  g_depth = fmaf((gtt + gtt) * qe, rtd, g_depth);
+  g_qe = fmaf(gtt * kLn2, l2d, g_qe);
+  // depth = max(ratio^expo, d_lb)
+  const float g_pw = (pw >= c.dlb) ? g_depth : 0.0f;
+  const float A = (g_pw * expo) * pw;                              // dL/d ln ratio
+  g_qe = fmaf(-((g_pw * pw) * (l2r * kLn2)), expo * expo, g_qe);   // d expo / d qe = -expo^2
+  // ratio = Q n (qe + 1) / (p sqrtS + 1e-8)
+  o.gQ = A * __builtin_amdgcn_rcpf(Q);
+  g_n = fmaf(A, s.inv_n, g_n);
+  g_qe = fmaf(A, __builtin_amdgcn_rcpf(qe1), g_qe);
+  g_p = fmaf(-A * s.sqrtS, rdd, g_p);
+  o.gn = g_n;
+  o.gq = g_qe;
+  o.gp = g_p;
+  return o;
+}
+
 }  // namespace ddr

@@ -107,6 +107,7 @@ __device__ __forceinline__ V opq(V x) {
   return x;
 }
 __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
+// 16-B runoff row segments (plain stores: measured faster than 8-B segments and than nt stores)
 __device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
@@ -434,7 +435,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   int ref[KR], off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
   unsigned up[KR];
-  R lam[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR];
+  R lam[KR], xc[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR];  // xc = x(t), xa = x(t-1), xb = x(t-2) prefetch
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -445,7 +446,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     dl[k] = a.s.dloc[P];
     up[k] = pack_up(a, P);
     lam[k] = R(0);
-    xa[k] = xb[k] = R(0);
+    xc[k] = xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
     if (hk) tab.put(r, load_static<R>(a, ref[k]));
   }
@@ -479,11 +480,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + (r < B.nloc ? r : 0)];
     }
   };
-  auto up_x = [&](int u, int tick, int64_t t) -> R {
-    if (u < B.nloc) {
-      const int tc = tick < 0 ? 0 : tick;
-      return xsave[xs_base + (int64_t)tc * B.nloc + u];
-    }
+  // x of upstream slot u at step t: a reach of this block (row of its tick, one load at a scalar
+  // base), or a virtual inflow (the forward's boundary granule)
+  auto up_x = [&](int u, const R* row, int64_t t) -> R {
+    if (u < B.nloc) return row[u];
     const int e = a.s.v_edge[B.virt0 + (u - B.nloc)];
     const int64_t tt = t < 0 ? 0 : t;
     return R(a.bnd[(int64_t)e * T + tt]);
@@ -492,6 +492,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // xp = x(t-1) of the step each reach runs at this tick; xn receives x(t-2) for the next tick
   auto tick = [&](int tb, R(&xp)[KR], R(&xn)[KR]) {
     const int tau = TT - 1 - tb;  // forward tick
+    const R* xrow1 = xsave + xs_base + (int64_t)(tau >= 1 ? tau - 1 : 0) * B.nloc;  // x(t-1) of this block
+    const R* xrow2 = xsave + xs_base + (int64_t)(tau >= 2 ? tau - 2 : 0) * B.nloc;  // x(t-2)
+    const R* grow = gsch + xs_base + (int64_t)tau * B.nloc;
+    const R* qrow = qsb + (int64_t)tau * B.nloc;
     const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -556,22 +560,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int t = tau - off[k];
       const bool active = hk && t >= 1 && t < T;
       const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const R xtk = xsave[xs_base + (int64_t)tau * B.nloc + rs];  // own x(t)
-      const R gk = gsch[xs_base + (int64_t)tau * B.nloc + rs];    // dL/dQ_t (expand_grad_kernel)
-      const R qvk = qsb[(int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale (mmc.py:303-304)
-      const R xu0 = up_x(up_0(up[k]), tau - 1, tcl);
-      const R xu1 = up_x(up_1(up[k]), tau - 1, tcl);
-      const R xup0 = up_x(up_0(up[k]), tau - 2, tcl - 1);
-      const R xup1 = up_x(up_1(up[k]), tau - 2, tcl - 1);
+      const R xtk = xc[k];                 // own x(t) (kept from the previous tick)
+      const R gk = grow[rs];               // dL/dQ_t (expand_grad_kernel)
+      const R qvk = qrow[rs];              // q'[t-1] * flow_scale (mmc.py:303-304)
+      const R xu0 = up_x(up_0(up[k]), xrow1, tcl);
+      const R xu1 = up_x(up_1(up[k]), xrow1, tcl);
+      const R xup0 = up_x(up_0(up[k]), xrow2, tcl - 1);
+      const R xup1 = up_x(up_1(up[k]), xrow2, tcl - 1);
       const ReachStatic<R> st = tab.template get<true>(rs);
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
       const double gb64 = (double)gx + A[k];             // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
       const R gb = R(gb64);
       const R Qp = (t == 1 && carry) ? xp[k] : rmax(xp[k], cs.qlb);
-      R c1, c2, c3, c4, tw, ss;
-      Geom<R> geo;
-      coefficients<R, true>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
       const int nup = up_n(up[k]);
       R Sx = R(0), I = R(0);
       const bool c0 = (t == 1 && carry);
@@ -584,15 +585,23 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int b = a.s.upb[P], c = a.s.upc[P];
         for (int j = 2; j < c; ++j) {
           const int u = a.s.uplist[b + j];
-          Sx = Sx + up_x(u, tau - 1, t);
-          const R xj = up_x(u, tau - 2, t - 1);
+          Sx = Sx + up_x(u, xrow1, t);
+          const R xj = up_x(u, xrow2, t - 1);
           I = I + (c0 ? xj : rmax(xj, cs.qlb));
         }
       }
-      const R qc = rmax(qvk, cs.qlb);
-      const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
-      R gQ, gn, gq, gp;
-      coefficients_vjp<R, true>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+      R c1, c2, c3, gQ, gn, gq, gp;
+      if constexpr (std::is_same<R, float>::value) {
+        const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
+        c1 = o.c1; c2 = o.c2; c3 = o.c3; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
+      } else {
+        R c4, tw, ss;
+        Geom<R> geo;
+        coefficients<R, true>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
+        const R qc = rmax(qvk, cs.qlb);
+        const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
+        coefficients_vjp<R, true>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+      }
       if (active) {
         pn[k] = pn[k] + gn;
         pq[k] = pq[k] + gq;
@@ -617,13 +626,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2
+  load_own(TT - 1, xc, tid);
   load_own(TT - 2, xa, tid);
 #pragma unroll 1
   for (int tb = 0; tb < TT; ++tb) {
     if (a.prof && tid == 0) prof_tick(a.prof, tb);
     tick(tb, xa, xb);
 #pragma unroll
-    for (int k = 0; k < KR; ++k) xa[k] = xb[k];
+    for (int k = 0; k < KR; ++k) {
+      xc[k] = xa[k];
+      xa[k] = xb[k];
+    }
   }
   if (a.prof && tid == 0) prof_end(a.prof, prof_wait);
 }
