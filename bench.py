@@ -82,6 +82,20 @@ def cpu_baseline(args):
                       f"spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve), {el:.1f} s"}
 
 
+def measured_traffic(kernel: str, args) -> float | None:
+    """HBM bytes per launch of `kernel` from the committed PMC measurement (profiles/), if it was taken
+    on this workload; None otherwise (rocprofv3 counters cannot be read from inside the run)."""
+    f = ROOT / "profiles" / "r01_traffic_c5.json"
+    try:
+        d = json.loads(f.read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("config") != {"reaches_per_gpu": args.reaches, "T": args.T} or args.dtype != "f32":
+        return None
+    k = d["kernels"].get(kernel)
+    return None if k is None else float(k["bytes_per_launch"])
+
+
 def block_profile(path, g, step, lib):
     """One extra step with the per-workgroup profile on: start/end/import-wait per block (µs)."""
     nb = g.info.n_blocks
@@ -122,8 +136,8 @@ def main():
     ap.add_argument("--T", type=int, default=8760)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--cpu-reaches", type=int, default=20_000)
-    ap.add_argument("--cpu-T", type=int, default=240)
+    ap.add_argument("--cpu-reaches", type=int, default=40_000)
+    ap.add_argument("--cpu-T", type=int, default=720)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
     args = ap.parse_args()
@@ -251,8 +265,10 @@ def main():
                        "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
                        "cut_edges_rank0": g.info.n_cut, "parallelism": f"basin-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": f"route_{dom}_kernel",
-                         "bytes_per_reach_step": FWD_BYTES if dom == "forward" else BWD_BYTES},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic(f"route_{dom}_kernel", args),
+                         "kernel": f"route_{dom}_kernel",
+                         "bytes_per_reach_step": FWD_BYTES if dom == "forward" else BWD_BYTES,
+                         "note": "VALU-issue bound, not HBM bound: see DESIGN.md section 4"},
             "kernels": kern,
             "cpu_baseline": cpu,
         }

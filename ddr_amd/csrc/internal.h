@@ -35,7 +35,7 @@ constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
 constexpr int kChunk = DDR_CHUNK;
 // Parameter-gradient partial sums are flushed to the fp64 accumulators every kGradFlush steps
 // (aligned to the step index, so the summation grouping does not depend on the partition).
-constexpr int kGradFlush = 32;
+constexpr int kGradFlush = 128;
 // Transpose tiles (reaches) between the (reach, step) layouts of the API and the tick-major
 // schedule layout.
 constexpr int kTileR = 64;
