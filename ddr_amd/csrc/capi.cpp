@@ -1,5 +1,6 @@
 // C ABI of libddr_mc.so (include/ddr_mc.h).  No exception crosses this boundary; errors are
 // returned as ddr_status codes with a thread-local message (ddr_last_error).
+#include <cmath>
 #include <cstring>
 #include <exception>
 #include <string>
@@ -89,6 +90,7 @@ void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr
   a.c[6] = c->side_slope_lb;
   a.c[7] = c->side_slope_ub;
   for (int i = 0; i < 8; ++i) a.cf[i] = (float)a.c[i];
+  a.ln_dlb = std::log(sizeof(R) == 4 ? (double)a.cf[4] : a.c[4]);
 }
 
 template <typename R>

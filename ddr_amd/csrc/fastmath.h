@@ -122,14 +122,12 @@ __device__ __forceinline__ void div_rn_np(const float (&a)[NP], const float (&b)
   DDR_FOR_NP q[h] = fmaf(r[h], y[h], q[h]);
 }
 
+// ln x (fp64, table-driven as ln_tab) for NP values in lockstep
 template <int NP>
-__device__ __forceinline__ void pow_pos_np(const float (&x)[NP], const float (&y)[NP], float (&out)[NP],
-                                           const PowK& K) {
+__device__ __forceinline__ void ln_np(const float (&x)[NP], double (&l)[NP], const PowK& K) {
   const double2* lt = reinterpret_cast<const double2*>(math_lds());
-  const double* et = math_lds() + 2 * kLnTabN;
-  double m[NP], r[NP], t[NP], de[NP], l[NP], z[NP], kd[NP];
+  double m[NP], r[NP], t[NP], de[NP];
   double2 cl[NP];
-  int k[NP];
   DDR_FOR_NP {
     const unsigned bits = __float_as_uint(x[h]);
     de[h] = (double)((int)(bits >> 23) - 127);
@@ -143,7 +141,14 @@ __device__ __forceinline__ void pow_pos_np(const float (&x)[NP], const float (&y
   DDR_FOR_NP t[h] = fma(t[h], r[h], -0.5);
   DDR_FOR_NP t[h] = fma(t[h], r[h] * r[h], r[h]);
   DDR_FOR_NP l[h] = fma(de[h], K.ln2hi, fma(de[h], K.ln2lo, cl[h].y + t[h]));
-  DDR_FOR_NP z[h] = (double)y[h] * l[h];
+}
+
+// exp z (fp64, table-driven as exp_tab) for NP values in lockstep; E receives the fp64 result
+template <int NP>
+__device__ __forceinline__ void exp_np(const double (&z)[NP], double (&E)[NP], const PowK& K) {
+  const double* et = math_lds() + 2 * kLnTabN;
+  double r[NP], t[NP], kd[NP];
+  int k[NP];
   DDR_FOR_NP kd[h] = __builtin_rint(z[h] * K.invl);
   DDR_FOR_NP k[h] = (int)kd[h];
   DDR_FOR_NP r[h] = fma(-kd[h], K.llo, fma(-kd[h], K.lhi, z[h]));
@@ -152,7 +157,17 @@ __device__ __forceinline__ void pow_pos_np(const float (&x)[NP], const float (&y
   DDR_FOR_NP t[h] = fma(t[h], r[h], 0.5);
   DDR_FOR_NP t[h] = fma(t[h], r[h], 1.0);
   DDR_FOR_NP t[h] = fma(t[h], r[h], 1.0);
-  DDR_FOR_NP out[h] = (float)__builtin_amdgcn_ldexp(et[k[h] & 127] * t[h], k[h] >> 7);
+  DDR_FOR_NP E[h] = __builtin_amdgcn_ldexp(et[k[h] & 127] * t[h], k[h] >> 7);
+}
+
+template <int NP>
+__device__ __forceinline__ void pow_pos_np(const float (&x)[NP], const float (&y)[NP], float (&out)[NP],
+                                           const PowK& K) {
+  double l[NP], z[NP], E[NP];
+  ln_np<NP>(x, l, K);
+  DDR_FOR_NP z[h] = (double)y[h] * l[h];
+  exp_np<NP>(z, E, K);
+  DDR_FOR_NP out[h] = (float)E[h];
 }
 
 }  // namespace ddr

@@ -14,6 +14,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "fastmath.h"
 
 namespace ddr {
@@ -21,7 +23,8 @@ namespace ddr {
 template <typename R>
 struct Consts {
   R dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub;
-  PowK pk;  // fp64 constants of the fp32 pow (register-pinned by the routing kernels)
+  PowK pk;        // fp64 constants of the fp32 pow (register-pinned by the routing kernels)
+  double ln_dlb;  // ln of the depth lower bound (fp64, host-computed)
 };
 
 __device__ __forceinline__ float dv(float a, float b) { return div_rn(a, b); }
@@ -201,11 +204,30 @@ __device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], c
   DDR_FOR_NP a[h] = (Q[h] * s[h].n) * s[h].qe1();
   DDR_FOR_NP b[h] = s[h].dd;
   dv_np<NP>(a, b, ratio);
-  DDR_FOR_NP e[h] = s[h].expo;
-  pw_np<NP>(ratio, e, depth, c.pk);
-  DDR_FOR_NP depth[h] = rmax(depth[h], c.dlb);
-  DDR_FOR_NP e[h] = s[h].qe;
-  pw_np<NP>(depth, e, dq, c.pk);
+  if constexpr (std::is_same<R, float>::value) {
+    // pw = ratio^expo and dq = depth^qe share one logarithm: for depth = pw, ln(pw) is derived from
+    // the exponent z = expo ln(ratio) and the fp64 value E of the first pow, ln(pw) = z + ln(pw / E)
+    // with |pw / E - 1| < 2^-24 (two terms of log1p); for depth = d_lb the constant ln(d_lb).
+    double l[NP], z[NP], E[NP];
+    ln_np<NP>(ratio, l, c.pk);
+    DDR_FOR_NP z[h] = (double)s[h].expo * l[h];
+    exp_np<NP>(z, E, c.pk);
+    DDR_FOR_NP {
+      const float pw = (float)E[h];
+      depth[h] = rmax(pw, c.dlb);
+      const double u = ((double)pw - E[h]) * __builtin_amdgcn_rcp(E[h]);
+      l[h] = (pw >= c.dlb) ? z[h] + fma(-0.5 * u, u, u) : c.ln_dlb;
+      z[h] = (double)s[h].qe * l[h];
+    }
+    exp_np<NP>(z, E, c.pk);
+    DDR_FOR_NP dq[h] = (float)E[h];
+  } else {
+    DDR_FOR_NP e[h] = s[h].expo;
+    pw_np<NP>(ratio, e, depth, c.pk);
+    DDR_FOR_NP depth[h] = rmax(depth[h], c.dlb);
+    DDR_FOR_NP e[h] = s[h].qe;
+    pw_np<NP>(depth, e, dq, c.pk);
+  }
   DDR_FOR_NP o[h].tw = s[h].p * dq[h];
   DDR_FOR_NP a[h] = o[h].tw * s[h].qe;
   DDR_FOR_NP b[h] = R(2) * depth[h];

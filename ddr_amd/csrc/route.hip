@@ -72,11 +72,11 @@ __device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a) {
 #define DDR_PIN_POWK 1
 #endif
   return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7],
-                       DDR_PIN_POWK ? pow_consts_vgpr() : pow_consts()};
+                       DDR_PIN_POWK ? pow_consts_vgpr() : pow_consts(), a.ln_dlb};
 }
 template <>
 __device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a) {
-  return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7], pow_consts()};
+  return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7], pow_consts(), a.ln_dlb};
 }
 
 template <typename R>
@@ -221,7 +221,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   R ob0[KR], ob1[KR], ob2[KR], ob3[KR];
   R* runoff = static_cast<R*>(a.runoff);
   const bool emit = runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
-  const bool emit4 = (T & 3) == 0;  // rows 16-B aligned: vector stores
+  // rows 16-B aligned: vector stores (per-step 4-B stores measured 1.6x slower for the whole kernel)
+  const bool emit4 = (T & 3) == 0;
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -712,9 +713,15 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
 // Tiles of kTileR reaches x TrSteps<R> steps, 1024 threads, 16 elements per thread: the (reach,
 // step) side moves whole rows of TrSteps steps per reach (1 KiB), the schedule side runs of
 // positions of one tick offset; the tile (~66 KiB) is staged in LDS.
+#ifndef DDR_TR_ROW
+#define DDR_TR_ROW 1024
+#endif
+#ifndef DDR_TR_THREADS
+#define DDR_TR_THREADS 1024
+#endif
 template <typename R>
-constexpr int TrSteps = 1024 / sizeof(R);
-constexpr int kTrThreads = 1024;
+constexpr int TrSteps = DDR_TR_ROW / sizeof(R);
+constexpr int kTrThreads = DDR_TR_THREADS;
 
 // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
 template <typename R>

@@ -43,6 +43,7 @@ struct RouteArgs {
   unsigned long long* prof;  // debug per-workgroup profile (ddr_set_block_profile), or null
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
   float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
+  double ln_dlb;  // ln of the fp32-rounded depth lower bound (fp32 pow derivation, physics.h)
 };
 
 struct GaugeArgs {
