@@ -1,0 +1,159 @@
+"""Parity at BASELINE.json's full sizes (C2: 5k reaches x 8760 h; C5: 800k reaches x 8760 h).
+
+The oracle cannot route 800k reaches over a water year in seconds, so the full-size checks use the
+properties the domain offers:
+
+* **Basin independence + oracle on samples.** Outlet basins do not interact, so a basin's discharge and
+  its reaches' parameter gradients inside the full C5 forest must equal the oracle routing that basin
+  alone.  The samples include a basin the partitioner split across several workgroups (cut edges,
+  cross-block hand-off over all 8760 steps) and small single-block basins.
+* **Partition invariance at full size.** The same multi-block basin routed alone (a different
+  workgroup split) gives bitwise the same discharge and gradients as inside the 800k forest.
+* **C2 end to end.** The whole 5k-reach Hack-law basin over 8760 h against the oracle (fp32 recipe,
+  bitwise expected), which also pins the hot start and the clamp path over a full seasonal cycle.
+
+Tolerances as in test_gpu_route.py: fp32 kernel vs fp32 oracle max-rel <= 1e-6 (observed 0);
+gradients vs the fp64 oracle adjoint norm-rel <= 5e-5 (the fp32 adjoint's own rounding).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import maxrel, normrel
+from ddr_amd import synthetic
+from ddr_amd.graph import RiverGraph
+from ddr_amd.ops import RouteConsts, route
+from ddr_amd.partition import basin_labels, extract_basins
+from oracle import mc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RANGES = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
+T_FULL = 8760
+
+
+def _physical(u):
+    """denormalize (utils.py:166-185) in fp32 on the host; the kernel is fed exactly these values."""
+    n = (u["n"] * np.float32(RANGES["n"][1] - RANGES["n"][0]) + np.float32(RANGES["n"][0])).astype(np.float32)
+    q = (u["q_spatial"] * np.float32(1.0) + np.float32(0.0)).astype(np.float32)
+    lo, hi = np.log(np.float32(1.0 + 1e-6)), np.log(np.float32(200.0))
+    p = np.exp(u["p_spatial"] * np.float32(hi - lo) + np.float32(lo)).astype(np.float32)
+    return n, q, p
+
+
+class FullForest:
+    """One synthetic network resident on the device, routed fwd+bwd once; per-reach inputs kept on host."""
+
+    def __init__(self, net, seed, dev, T=T_FULL, **gkw):
+        self.net, self.T, self.dev = net, T, dev
+        at = synthetic.reach_attributes(net.n, seed)
+        u = synthetic.unit_parameters(net.n, seed)
+        self.n, self.q, self.p = _physical(u)
+        self.length, self.slope, self.x = at.length, np.maximum(at.slope, np.float32(1e-3)), at.x
+        self.qprime = synthetic.lateral_inflow_torch(net.n, T, seed=seed, device=dev)
+        gen = torch.Generator(device=dev).manual_seed(seed + 4000)
+        self.W = torch.rand((net.n, T), device=dev, dtype=torch.float32, generator=gen)
+        self.graph = RiverGraph(net.n, net.rows, net.cols, **gkw)
+        self.run(self.graph, np.arange(net.n))
+
+    def run(self, graph, ids):
+        tt = lambda a: torch.from_numpy(np.ascontiguousarray(a[ids])).to(self.dev)  # noqa: E731
+        n, q, p = (tt(a).requires_grad_(True) for a in (self.n, self.q, self.p))
+        full = len(ids) == self.net.n
+        qp = self.qprime if full else self.qprime[:, torch.from_numpy(ids).to(self.dev)].contiguous()
+        W = self.W if full else self.W[torch.from_numpy(ids).to(self.dev)].contiguous()
+        runoff, _, _, _ = route(graph, qp, n, q, p, tt(self.length), tt(self.slope), tt(self.x),
+                                consts=RouteConsts())
+        runoff.backward(W)
+        torch.cuda.synchronize()
+        out = {"runoff": runoff.detach(), "gn": n.grad, "gq": q.grad, "gp": p.grad}
+        if full:
+            self.out = out
+        return out
+
+    def basin(self, ids):
+        """Subnetwork (topologically ordered COO) of the reaches `ids` (sorted, whole basins)."""
+        keep = np.zeros(self.net.n, bool)
+        keep[ids] = True
+        ns, rs, cs, sel = extract_basins(self.net.n, self.net.rows, self.net.cols, keep)
+        assert np.array_equal(sel, ids)
+        return ns, rs, cs
+
+    def oracle(self, ids, grads=True):
+        ns, rs, cs = self.basin(ids)
+        net = O.Network.from_coo(ns, rs, cs)
+        r = O.Reaches(self.n[ids], self.q[ids], self.p[ids], self.length[ids], self.slope[ids], self.x[ids])
+        qp = self.qprime[:, torch.from_numpy(ids).to(self.dev)].cpu().numpy()
+        ref = O.route(net, r, qp, O.Bounds(), dtype=np.float32)
+        if grads:
+            W = self.W[torch.from_numpy(ids).to(self.dev)].cpu().numpy()
+            ref["grads"] = O.route_backward(net, r, qp, ref["x"], W, O.Bounds())
+        return ref
+
+
+@pytest.fixture(scope="module")
+def c5(cuda):
+    net = synthetic.forest(synthetic.zipf_sizes(800_000, 3000, 0.35), seed=5, single_inflow=0.35)
+    ff = FullForest(net, 5, cuda)
+    yield ff
+    del ff.qprime, ff.W, ff.out
+    torch.cuda.empty_cache()
+
+
+def _basins_by_blocks(ff):
+    s = ff.graph.structure()
+    lab = basin_labels(ff.net.n, ff.net.rows, ff.net.cols)
+    order = np.argsort(lab, kind="stable")
+    starts = np.r_[0, np.flatnonzero(np.diff(lab[order])) + 1]
+    members = np.split(order, starts[1:])
+    nblk = np.array([len(np.unique(s["block"][m])) for m in members])
+    return members, nblk
+
+
+def test_c5_multiblock_basin_matches_oracle_and_is_partition_invariant(c5):
+    members, nblk = _basins_by_blocks(c5)
+    assert c5.graph.info.n_cut > 0
+    multi = [i for i in range(len(members)) if nblk[i] >= 2]
+    assert multi, "no basin of the C5 forest spans several workgroups"
+    b = min(multi, key=lambda i: len(members[i]))  # the smallest split basin keeps the oracle fast
+    ids = np.sort(members[b])
+    ref = c5.oracle(ids, grads=False)
+    got = c5.out["runoff"][torch.from_numpy(ids).to(c5.dev)].cpu().numpy()
+    assert maxrel(got, ref["runoff"]) <= 1e-6
+    # the same basin alone: a different partition, bitwise-identical discharge and gradients
+    ns, rs, cs = c5.basin(ids)
+    alone = c5.run(RiverGraph(ns, rs, cs), ids)
+    np.testing.assert_array_equal(alone["runoff"].cpu().numpy(), got)
+    sel = torch.from_numpy(ids).to(c5.dev)
+    for k in ("gn", "gq", "gp"):
+        np.testing.assert_array_equal(alone[k].cpu().numpy(), c5.out[k][sel].cpu().numpy())
+
+
+def test_c5_small_basins_match_oracle_with_gradients(c5):
+    members, nblk = _basins_by_blocks(c5)
+    sizes = np.array([len(m) for m in members])
+    rng = np.random.default_rng(0)
+    cand = np.flatnonzero((sizes >= 20) & (sizes <= 400))
+    pick = rng.choice(cand, size=min(4, len(cand)), replace=False)
+    ids = np.sort(np.concatenate([members[i] for i in pick]))
+    ref = c5.oracle(ids)
+    sel = torch.from_numpy(ids).to(c5.dev)
+    assert maxrel(c5.out["runoff"][sel].cpu().numpy(), ref["runoff"]) <= 1e-6
+    for k, rk in (("gn", "n"), ("gq", "q_spatial"), ("gp", "p_spatial")):
+        assert normrel(c5.out[k][sel].cpu().numpy(), ref["grads"][rk]) <= 5e-5, k
+
+
+def test_c5_outputs_finite_and_bounded(c5):
+    r = c5.out["runoff"]
+    assert r.shape == (800_000, T_FULL)
+    assert bool(torch.isfinite(r).all()) and float(r.min()) >= np.float32(1e-4)
+    for k in ("gn", "gq", "gp"):
+        assert bool(torch.isfinite(c5.out[k]).all()), k
+
+
+def test_c2_full_water_year_matches_oracle(cuda):
+    net = synthetic.hack_basin(5000, seed=2)
+    ff = FullForest(net, 2, cuda)
+    ref = ff.oracle(np.arange(net.n), grads=False)
+    assert maxrel(ff.out["runoff"].cpu().numpy(), ref["runoff"]) <= 1e-6
