@@ -6,9 +6,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export DDR_CHECK_STATUS=1
-timeout -k 10 600 python -m pytest $R/tests -q -m gpu -x > $OUT/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest $R/tests -v -m gpu -x --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?
-grep -E "passed|failed|FAILED|^E  " $OUT/pytest.log | cut -c1-300 | head -20
+grep -E "passed|failed|FAILED|PASSED|^E  " $OUT/pytest.log | cut -c1-300 | head -60
 [ $rc -ne 0 ] && { echo "PYTEST FAILED rc=$rc"; exit $rc; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/bench.log 2>&1
