@@ -38,7 +38,10 @@ constexpr int kChunk = DDR_CHUNK;
 constexpr int kGradFlush = 128;
 // Transpose tiles (reaches) between the (reach, step) layouts of the API and the tick-major
 // schedule layout.
-constexpr int kTileR = 64;
+#ifndef DDR_TILE_R
+#define DDR_TILE_R 256
+#endif
+constexpr int kTileR = DDR_TILE_R;
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 // LDS slots per buffer of the routing kernels: every block's nloc + nvirt slots, one zero slot

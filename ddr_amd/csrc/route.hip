@@ -714,7 +714,7 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
 // step) side moves whole rows of TrSteps steps per reach (1 KiB), the schedule side runs of
 // positions of one tick offset; the tile (~66 KiB) is staged in LDS.
 #ifndef DDR_TR_ROW
-#define DDR_TR_ROW 1024
+#define DDR_TR_ROW 256
 #endif
 #ifndef DDR_TR_THREADS
 #define DDR_TR_THREADS 1024
