@@ -906,7 +906,10 @@ hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t st
 template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream) {
   if (g->max_nloc == 0 || a.T == 0) return hipSuccess;
-  constexpr int G = sizeof(R) == 4 ? 8 : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
+#ifndef DDR_GATHER_G
+#define DDR_GATHER_G 8
+#endif
+  constexpr int G = sizeof(R) == 4 ? DDR_GATHER_G : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
   a.gather_steps = G;
   const size_t smem = (size_t)G * g->max_nloc * sizeof(R);
   auto kern = gather_qprime_kernel<R, G>;
