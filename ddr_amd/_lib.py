@@ -36,6 +36,8 @@ DDR_FWD_SAVE_X = 1
 DDR_FWD_CARRY = 2
 DDR_FWD_NO_RUNOFF = 4
 
+DDR_DEBUG_FORCE_TIMEOUT = 1
+
 
 class BuildOpts(C.Structure):
     _fields_ = [("flags", C.c_int32), ("max_block_reaches", C.c_int32), ("target_blocks", C.c_int32),
@@ -46,7 +48,7 @@ class GraphInfo(C.Structure):
     _fields_ = [(name, C.c_int64) for name in (
         "n", "nnz", "n_basins", "n_pieces", "n_blocks", "n_cut", "max_depth", "max_block_depth",
         "reaches_per_thread", "save_elems_per_t", "save_elems_fixed", "bnd_elems_per_t", "bwd_elems_per_t",
-        "bwd_elems_fixed", "status_bytes")]
+        "bwd_elems_fixed", "status_bytes", "generations")]
 
 
 class Consts(C.Structure):
@@ -86,6 +88,8 @@ _SIGS = {
     "ddr_gauge_reduce_f32": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _P, _P]),
     "ddr_gauge_reduce_f64": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _P, _P]),
     "ddr_graph_status": (C.c_int, [_P, _P]),
+    "ddr_status_check": (C.c_int, [_I32]),
+    "ddr_set_debug_flags": (C.c_int, [_I32]),
     "ddr_tri_solve": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _P]),
     "ddr_tri_grad_values": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P]),
     "ddr_set_kernel_timing": (C.c_int, [_I32]),

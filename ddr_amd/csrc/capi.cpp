@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstring>
 #include <exception>
+#include <mutex>
 #include <string>
 
 #include "internal.h"
@@ -40,6 +41,67 @@ struct KernelTiming {
   bool recorded[2] = {false, false};
 } g_timing;
 unsigned long long* g_prof[2] = {nullptr, nullptr};
+int32_t g_debug = 0;  // ddr_set_debug_flags
+
+// Hand-off failures surface without a host sync on the hot path: after every routing launch the
+// status block's first words are copied (async, same stream) into a pinned slot with an event
+// behind it.  Every later entry point polls the completed slots and returns DDR_ERR_TIMEOUT for
+// a launch that timed out; ddr_status_check(1) waits for all of them.
+struct PendingStatus {
+  static constexpr int kSlots = 64;
+  std::mutex mu;
+  unsigned* host = nullptr;  // pinned, kSlots x 4 words
+  hipEvent_t ev[kSlots] = {};
+  const char* what[kSlots] = {};
+  int head = 0;
+  bool failed = false;
+  std::string msg;
+
+  void harvest(int k) {
+    const unsigned* w = host + 4 * k;
+    if (w[0] && !failed) {
+      failed = true;
+      msg = std::to_string(w[0]) + " inter-workgroup hand-offs of a " + what[k] +
+            " launch timed out (first logical block " + std::to_string((int)w[1] - 1) +
+            "); its outputs hold NaN";
+    }
+    (void)hipEventDestroy(ev[k]);
+    ev[k] = nullptr;
+  }
+  // caller holds mu
+  void poll(bool wait) {
+    for (int k = 0; k < kSlots; ++k) {
+      if (!ev[k]) continue;
+      if (wait) (void)hipEventSynchronize(ev[k]);
+      if (hipEventQuery(ev[k]) == hipSuccess) harvest(k);
+    }
+  }
+  ddr_status take_error() {
+    if (!failed) return DDR_OK;
+    failed = false;
+    return fail(DDR_ERR_TIMEOUT, msg);
+  }
+  ddr_status enqueue(const void* status, hipStream_t s, const char* which) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!host) DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), sizeof(unsigned) * 4 * kSlots, hipHostMallocDefault));
+    const int k = head;
+    head = (head + 1) % kSlots;
+    if (ev[k]) {
+      (void)hipEventSynchronize(ev[k]);
+      harvest(k);
+    }
+    DDR_HIP(hipMemcpyAsync(host + 4 * k, status, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    DDR_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    what[k] = which;
+    DDR_HIP(hipEventRecord(ev[k], s));
+    return DDR_OK;
+  }
+  ddr_status check(bool wait) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (host) poll(wait);
+    return take_error();
+  }
+} g_pending;
 
 hipError_t timing_mark(int which, int edge, hipStream_t s) {
   if (!g_timing.on) return hipSuccess;
@@ -93,14 +155,16 @@ void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr
   a.ln_dlb = std::log(sizeof(R) == 4 ? (double)a.cf[4] : a.c[4]);
 }
 
+// The routing kernels need no co-residency (ticket-ordered blocks, route.hip), only that one
+// workgroup fits a CU with the schedule's LDS.
 template <typename R>
-ddr_status check_resident(const Graph* g, bool backward) {
-  if (g->n_cut == 0) return DDR_OK;  // no inter-workgroup waits: any grid size is safe
+ddr_status check_launchable(const Graph* g, bool backward) {
   const int cap = max_resident_blocks<R>(g, backward);
   if (cap < 0) return fail(DDR_ERR_HIP, "occupancy query failed");
-  if ((int64_t)g->blocks.size() > cap)
-    return fail(DDR_ERR_CAPACITY, "schedule needs " + std::to_string(g->blocks.size()) +
-                                      " co-resident workgroups, device admits " + std::to_string(cap));
+  if (cap == 0)
+    return fail(DDR_ERR_CAPACITY, std::string("the ") + (backward ? "backward" : "forward") +
+                                      " routing kernel does not fit a CU at this schedule's LDS size" +
+                                      (sizeof(R) == 8 ? " (fp64: use a smaller max_block_reaches)" : ""));
   return DDR_OK;
 }
 
@@ -116,12 +180,13 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   if (!x_save) return fail(DDR_ERR_ARG, "x_save is required (routing state, and the staging of runoff)");
   if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: bnd buffer required");
   if (!status) return fail(DDR_ERR_ARG, "null status block");
-  if ((st = check_resident<R>(g, false))) return st;
+  if ((st = g_pending.check(false))) return st;
+  if ((st = check_launchable<R>(g, false))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bnd, 0xFF, sizeof(double) * g->n_cut * T, s));
   RouteArgs a;
-  fill_common<R>(a, g, c, r, T, qprime, flags);
+  fill_common<R>(a, g, c, r, T, qprime, flags | g_debug);
   a.q0 = q0;
   a.runoff = (flags & DDR_FWD_NO_RUNOFF) ? nullptr : runoff;
   a.x_save = x_save;
@@ -137,7 +202,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   DDR_HIP(launch_route<R>(g, a, false, s));
   DDR_HIP(timing_mark(0, 1, s));
   // runoff (N, T) is written by the routing kernel itself (16-B row segments every 4 steps)
-  return DDR_OK;
+  return g_pending.enqueue(status, s, "forward");
 }
 
 template <typename R>
@@ -153,13 +218,14 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   if (!bwd_bnd) return fail(DDR_ERR_ARG, "backward workspace required");
   if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
     return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
-  if ((st = check_resident<R>(g, true))) return st;
+  if ((st = g_pending.check(false))) return st;
+  if ((st = check_launchable<R>(g, true))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
   DDR_HIP(hipMemsetAsync(bwd_bnd + 2 * g->n_cut * T, 0, sizeof(double) * 3 * g->n, s));
   RouteArgs a;
-  fill_common<R>(a, g, c, r, T, qprime, flags);
+  fill_common<R>(a, g, c, r, T, qprime, flags | g_debug);
   a.x_save = const_cast<R*>(x_save);
   a.qs = const_cast<R*>(x_save) + (g->n * T + g->sum_dn);
   a.bnd = const_cast<double*>(bnd);
@@ -171,14 +237,12 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   a.gn = gn;
   a.gq = gq;
   a.gp = gp;
-  // workspace: [2 n_cut T f64 boundary][3 N f64 accumulators][grad in the schedule layout (R)]
-  a.gs = bwd_bnd + 2 * g->n_cut * T + 3 * g->n;
+  // workspace: [2 n_cut T f64 boundary][3 N f64 accumulators]; the kernel reads grad (N, T) itself
   a.prof = g_prof[1];
-  DDR_HIP(launch_expand_grad<R>(g, a, s));
   DDR_HIP(timing_mark(1, 0, s));
   DDR_HIP(launch_route<R>(g, a, true, s));
   DDR_HIP(timing_mark(1, 1, s));
-  return DDR_OK;
+  return g_pending.enqueue(status, s, "backward");
 }
 
 template <typename R>
@@ -251,6 +315,7 @@ ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
   info->bnd_elems_per_t = g->n_cut;
   info->bwd_elems_per_t = 2 * g->n_cut;
   info->bwd_elems_fixed = 3 * g->n;
+  info->generations = g->generations;
   info->status_bytes = kStatusBytes;
   return DDR_OK;
 }
@@ -314,6 +379,15 @@ ddr_status ddr_graph_status(const void* status, void* stream) {
   DDR_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   if (h[0]) return fail(DDR_ERR_TIMEOUT, std::to_string(h[0]) + " inter-workgroup hand-offs timed out (first block " +
                                              std::to_string((int)h[1] - 1) + ")");
+  return DDR_OK;
+}
+
+ddr_status ddr_status_check(int32_t wait) {
+  DDR_GUARD({ return g_pending.check(wait != 0); })
+}
+
+ddr_status ddr_set_debug_flags(int32_t flags) {
+  g_debug = (flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0;
   return DDR_OK;
 }
 

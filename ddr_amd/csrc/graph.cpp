@@ -122,6 +122,15 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   std::vector<char> is_root(n);
   std::vector<Piece> pieces;
   std::vector<int64_t> others;
+  // Workgroups take their logical block index from a ticket counter in block order (route.hip:
+  // take_ticket), and blocks are numbered by piece height, so a running workgroup's producers are
+  // running or done: a schedule with more blocks than resident workgroups is still deadlock-free.
+  // The packer first tries to fit one resident generation (all blocks co-resident, fully time-
+  // pipelined): path-weighted packing, then unweighted; failing both it packs gen x resident
+  // smaller blocks (every extra generation costs about T more ticks of the blocks it holds).
+  bool weighted = true;
+  int64_t gen = 1;
+  const int64_t cap_start = cap;
   for (;;) {
     // Stem-preserving split (bottom-up).  A reach whose subtree exceeds the capacity keeps its
     // deepest child (the main stem: every block boundary crossed along the longest flow path adds
@@ -209,7 +218,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     for (size_t p = 0; p < pieces.size(); ++p) {
       const int64_t r = pieces[p].root;
       const double L = (double)(ht[r] + g->dist[r] + kChunk * (hops_down[p] + pieces[p].height));
-      fac[p] = (steps + L) / steps;
+      fac[p] = weighted ? (steps + L) / steps : 1.0;
       wsum += (double)pieces[p].size * fac[p];
     }
     // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
@@ -225,7 +234,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     });
     int64_t ncut0 = 0;
     for (auto& P : pieces) ncut0 += (g->down[P.root] >= 0);
-    const int64_t limit = ncut0 > 0 ? std::min<int64_t>(target, resident) : target;
+    const int64_t limit = ncut0 > 0 ? std::min<int64_t>(target, resident) * gen : target;
     for (double capw = wsum / (double)limit;; capw *= 1.01) {
       load.clear();
       bcap.clear();
@@ -250,7 +259,9 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       if ((int64_t)load.size() <= limit || capw / 1.3 > (double)hard_cap) break;
     }
     const int64_t nblocks = (int64_t)load.size();
-    if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part] cap %ld hard %ld pieces %zu blocks %ld cut %ld\n", (long)cap, (long)hard_cap, pieces.size(), (long)nblocks, (long)ncut);
+    if (getenv("DDR_DEBUG_PART"))
+      fprintf(stderr, "[part] cap %ld hard %ld gen %ld weighted %d pieces %zu blocks %ld cut %ld\n", (long)cap,
+              (long)hard_cap, (long)gen, (int)weighted, pieces.size(), (long)nblocks, (long)ncut);
     {
       // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if two
       // workgroups would no longer fit on a CU
@@ -273,20 +284,29 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld lds %zu\n", (long)ms, (long)mv, (long)mc, need);
       if (need > kLdsBudget) {
         if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
-        hard_cap -= hard_cap / 8;
+        hard_cap -= std::max<int64_t>(1, hard_cap / 32);
         cap = std::min(cap, hard_cap);
         continue;
       }
     }
-    if (ncut > 0 && nblocks > resident) {
-      if (cap >= hard_cap) {
-        return fail(DDR_ERR_CAPACITY, "graph needs " + std::to_string(nblocks) +
-                                          " co-resident workgroups but the device admits " +
-                                          std::to_string(resident));
+    if (ncut > 0 && nblocks > limit) {
+      if (cap < hard_cap) {
+        cap = std::min<int64_t>(hard_cap, cap + cap / 32 + 1);
+        continue;
       }
-      cap = std::min<int64_t>(hard_cap, cap + cap / 32 + 1);
+      if (weighted) {
+        weighted = false;
+        cap = cap_start;
+        continue;
+      }
+      if (++gen > 64) return fail(DDR_ERR_CAPACITY, "graph cannot be packed into workgroups");
+      weighted = true;
+      const int64_t per_gen = std::min<int64_t>(target, resident) * gen;
+      cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + per_gen - 1) / per_gen));
       continue;
     }
+    g->generations = gen;
+    g->resident = resident;
     // ---- emit the schedule ---------------------------------------------------------------
     g->n_pieces = (int64_t)pieces.size();
     g->n_cut = ncut;
@@ -413,14 +433,6 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     }
     if ((st = upload(g.get(), &D.rs_loc, rs_loc))) return st;
     if ((st = upload(g.get(), &D.rs_ref, rs_ref))) return st;
-    std::vector<int32_t> rtile;
-    for (int64_t b = 0; b < nblocks; ++b)
-      for (int32_t r0 = 0; r0 < g->blocks[b].nloc; r0 += kTileR) {
-        rtile.push_back((int32_t)b);
-        rtile.push_back(r0);
-      }
-    g->n_rtiles = (int64_t)rtile.size() / 2;
-    if ((st = upload(g.get(), &D.rtile, rtile))) return st;
     break;
   }
   *out = g.release();

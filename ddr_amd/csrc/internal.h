@@ -23,8 +23,9 @@ namespace ddr {
 constexpr int kBlockThreads = DDR_BLOCK_THREADS;
 constexpr int kMaxKR = 4;
 constexpr int kBlocksPerCU = 1024 / kBlockThreads;
-// Default workgroup capacity (reaches), leaving LDS room for virtual inflows.
-constexpr int kDefaultBlockReaches = kBlockThreads * 15 / 4;
+// Default workgroup capacity (reaches): KR = 4 reaches per thread.  The LDS check of the builder
+// lowers it when a block's slots and import rings would not fit.
+constexpr int kDefaultBlockReaches = kBlockThreads * kMaxKR;
 // LDS budget per workgroup (160 KiB per CU).
 constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
 // Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").  Every
@@ -36,13 +37,6 @@ constexpr int kChunk = DDR_CHUNK;
 // Parameter-gradient partial sums are flushed to the fp64 accumulators every kGradFlush steps
 // (aligned to the step index, so the summation grouping does not depend on the partition).
 constexpr int kGradFlush = 128;
-// Transpose tiles (reaches) between the (reach, step) layouts of the API and the tick-major
-// schedule layout.
-#ifndef DDR_TILE_R
-#define DDR_TILE_R 256
-#endif
-constexpr int kTileR = DDR_TILE_R;
-
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 // LDS slots per buffer of the routing kernels: every block's nloc + nvirt slots, one zero slot
 // (missing upstreams of the forward read it), rounded up to even (16-B aligned statics rows).
@@ -50,12 +44,12 @@ __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_sl
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
 //   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64
-//   backward: A slots (f64) | B slots (R) | 6 statics (R) | ring [ncout][kChunk][2] f64
+//   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunk][2] (R)
 // (after the math tables of fastmath.h, which occupy the first kMathTabBytes)
 constexpr size_t kMathTabBytes = 3072;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nring, bool backward, size_t rsize) {
-  const size_t base = backward ? slots * (8 + rsize + 6 * rsize) : slots * (8 + 6 * rsize);
-  return kMathTabBytes + align16(base) + nring * kChunk * (backward ? 16 : 8);
+  const size_t base = backward ? slots * 9 * rsize : slots * (8 + 6 * rsize);
+  return kMathTabBytes + align16(base) + nring * kChunk * (backward ? 2 * rsize : 8);
 }
 
 // One workgroup's slice of the schedule.  Reaches of a block occupy internal positions
@@ -88,7 +82,6 @@ struct DevSchedule {
   int32_t* cout_loc = nullptr; // per block list: local indices of reaches with cut >= 0
   int32_t* pos_of_ref = nullptr;   // (N) internal position of each reference reach
   int32_t* block_of_pos = nullptr; // (N) block of each internal position
-  int32_t* rtile = nullptr;        // (n_rtiles, 2) tiles of kTileR reaches: (block, first local index)
   int32_t* rs_loc = nullptr;       // (N) per block, local indices in ascending reference order
   int32_t* rs_ref = nullptr;       // (N) the matching reference indices
 };
@@ -105,7 +98,8 @@ struct Graph {
   std::vector<BlockDesc> blocks;
   int64_t sum_dn = 0;    // sum over blocks of dmax * nloc
   int max_nloc = 0;      // largest block
-  int64_t n_rtiles = 0;  // tiles of kTileR reaches (never straddling a block) for the layout transposes
+  int64_t generations = 1;  // ceil(blocks / resident) the packer aimed for (1: all blocks co-resident)
+  int64_t resident = 0;     // co-resident workgroups assumed by the packer
   DevSchedule dev;
   std::vector<void*> allocations;
 };
@@ -127,7 +121,14 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
                        const ddr_build_opts* opts, Graph** out);
 void destroy_graph(Graph* g);
 
-// status block layout (device): word 0 = timeout count, word 1 = first failing block + 1
+// Status block layout (device, zeroed before every launch): word 0 = timed-out hand-offs, word 1 =
+// first failing block + 1, word 2 = forward ticket counter, word 3 = backward ticket counter.
+// Workgroups take their logical block from the ticket counter (route.hip: take_ticket), so a
+// running workgroup's producers are always running or finished: any grid size is deadlock-free.
 constexpr int64_t kStatusBytes = 256;
+constexpr int kStatusTicketFwd = 2;
+constexpr int kStatusTicketBwd = 3;
+// RouteArgs.flags bits beyond the public DDR_FWD_* flags
+constexpr int32_t kFlagForceTimeout = 1 << 16;  // debug: every inter-workgroup wait times out
 
 }  // namespace ddr

@@ -83,6 +83,11 @@ __device__ __forceinline__ float rmax(float a, float b) { return __builtin_amdgc
 __device__ __forceinline__ float rmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
 __device__ __forceinline__ float rclamp(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 
+// torch.clamp(min=) with its NaN propagation (v_med3_f32 would return the bound for a NaN): used for
+// the routed state and the outputs, so that a failed hand-off's NaN reaches the caller.
+template <typename R>
+__device__ __forceinline__ R rmax_nan(R x, R lb) { return x < lb ? lb : x; }
+
 // torch: pow(R, 2 / 3) -- the Python double 2/3 is rounded to the tensor dtype.
 template <typename R>
 __device__ __forceinline__ R two_thirds() { return R(2.0 / 3.0); }

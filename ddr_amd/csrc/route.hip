@@ -10,11 +10,17 @@
 // are their own ready flag (sentinel = all ones, re-initialised before every launch), imported in
 // chunks of kChunk ticks so the hand-off latency is paid once per chunk.
 //
-// Each thread owns KR <= 4 reaches (r = tid + k * 512); two 512-thread workgroups share a CU
-// (4 waves per SIMD), so one workgroup's barrier wait is filled by the other's work.  The per-reach
-// statics live in LDS; registers hold only the per-reach state (Q, I, lambda, partial gradients)
-// and one tick of prefetched inputs.  Each tick: compute (reads upstream slots) -> barrier ->
-// publish (own slot) -> barrier.
+// Workgroups take their logical block from a ticket counter (take_ticket): blocks are numbered in
+// piece-height order, so the producers of a running workgroup were taken by workgroups that are
+// running or finished, whatever the grid size and the dispatch order.  A schedule with more blocks
+// than resident workgroups therefore runs to completion (as "generations"); one that fits runs
+// fully time-pipelined.  Every wait is bounded: a timeout records the device status word and yields
+// NaN, so a failed hand-off can never pass for a number (capi.cpp reports it as DDR_ERR_TIMEOUT).
+//
+// Each thread owns KR <= 4 reaches (r = tid + k * 1024); one 1024-thread workgroup per CU (4 waves
+// per SIMD).  The per-reach statics live in LDS; registers hold only the per-reach state and one
+// tick of prefetched inputs.  Each tick: compute (reads upstream slots) -> barrier -> publish (own
+// slot) -> barrier.
 //
 // Reference semantics (file:line in /root/reference):
 //   forward  src/ddr/routing/mmc.py:365-443, 487-559, 25-66; routing/utils.py:587-600 (fp64 solve)
@@ -47,20 +53,55 @@ __device__ __forceinline__ unsigned long long load_granule(const double* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Spin until the granule is published (bounded; on timeout record it and return 0).
-__device__ double wait_granule(const double* p, unsigned* status) {
+// Spin until the granule is published (bounded).  On a timeout (or with the debug flag that forces
+// one) record it in the status block and return NaN: the corruption then shows in the outputs.
+__device__ double wait_granule(const double* p, unsigned* status, int bid, bool force_timeout) {
   unsigned long long v = load_granule(p);
   unsigned spins = 0;
-  while (v == kSentinel) {
+  while (v == kSentinel || force_timeout) {
+    if (force_timeout || ++spins > (1u << 24)) {
+      atomicAdd(status, 1u);
+      atomicCAS(status + 1, 0u, (unsigned)bid + 1u);
+      return __builtin_nan("");
+    }
     __builtin_amdgcn_s_sleep(2);
     v = load_granule(p);
-    if (++spins > (1u << 24)) {
-      atomicAdd(status, 1u);
-      atomicCAS(status + 1, 0u, blockIdx.x + 1u);
-      return 0.0;
-    }
   }
   return __longlong_as_double(v);
+}
+
+// Logical block of this workgroup: the next ticket of the launch (forward: blocks in piece-height
+// order, backward: the reverse).  A workgroup waits only on blocks of lower logical index, whose
+// tickets were taken by workgroups already running or finished: no co-residency assumption.
+// The block descriptor of logical block `bid`, forced into SGPRs (behind the ticket atomic the
+// compiler cannot prove the descriptor unclobbered and would load it per lane).
+__device__ __forceinline__ BlockDesc block_desc(const BlockDesc* blocks, int bid) {
+  const BlockDesc d = blocks[bid];
+  BlockDesc u;
+  u.pos0 = __builtin_amdgcn_readfirstlane(d.pos0);
+  u.nloc = __builtin_amdgcn_readfirstlane(d.nloc);
+  u.virt0 = __builtin_amdgcn_readfirstlane(d.virt0);
+  u.nvirt = __builtin_amdgcn_readfirstlane(d.nvirt);
+  u.cout0 = __builtin_amdgcn_readfirstlane(d.cout0);
+  u.ncout = __builtin_amdgcn_readfirstlane(d.ncout);
+  u.dmax = __builtin_amdgcn_readfirstlane(d.dmax);
+  u.pad = 0;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(d.pre_dn & 0xffffffffu));
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)d.pre_dn >> 32));
+  u.pre_dn = (int64_t)(((unsigned long long)hi << 32) | lo);
+  return u;
+}
+
+// `slot` is a scratch LDS word that nothing else uses before the second barrier.
+__device__ __forceinline__ int take_ticket(unsigned* status, int word, int nblocks, bool reverse, int* slot) {
+  if (threadIdx.x == 0) {
+    const int t = (int)atomicAdd(status + word, 1u);
+    *slot = reverse ? nblocks - 1 - t : t;
+  }
+  __syncthreads();
+  const int bid = __builtin_amdgcn_readfirstlane(*slot);
+  __syncthreads();
+  return bid;
 }
 
 // Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
@@ -121,19 +162,19 @@ __device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u
 // Debug per-workgroup profile (ddr_set_block_profile): start, end, import wait, hardware id.
 // Layout per workgroup: kProfWords uint64 = start, end, wait, hwid, then a timestamp every 1024 ticks.
 constexpr int kProfWords = 16;
-__device__ __forceinline__ void prof_begin(unsigned long long* p) {
-  p += kProfWords * blockIdx.x;
+__device__ __forceinline__ void prof_begin(unsigned long long* p, int bid) {
+  p += kProfWords * bid;
   p[0] = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
   const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   p[3] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
 }
-__device__ __forceinline__ void prof_tick(unsigned long long* p, int tick) {
+__device__ __forceinline__ void prof_tick(unsigned long long* p, int bid, int tick) {
   if ((tick & 1023) == 0 && (tick >> 10) < kProfWords - 4)
-    p[kProfWords * blockIdx.x + 4 + (tick >> 10)] = __builtin_amdgcn_s_memrealtime();
+    p[kProfWords * bid + 4 + (tick >> 10)] = __builtin_amdgcn_s_memrealtime();
 }
-__device__ __forceinline__ void prof_end(unsigned long long* p, unsigned long long wait) {
-  p += kProfWords * blockIdx.x;
+__device__ __forceinline__ void prof_end(unsigned long long* p, int bid, unsigned long long wait) {
+  p += kProfWords * bid;
   p[1] = __builtin_amdgcn_s_memrealtime();
   p[2] = wait;
 }
@@ -195,19 +236,21 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #define DDR_FWD_NP 1
 #endif
   constexpr int NP = KR < DDR_FWD_NP ? KR : DDR_FWD_NP;  // slices whose physics runs in lockstep
-  const BlockDesc B = a.s.blocks[blockIdx.x];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int bid = take_ticket(a.status, kStatusTicketFwd, a.nblocks, false, reinterpret_cast<int*>(smem));
+  const BlockDesc B = block_desc(a.s.blocks, bid);
   const int tid = threadIdx.x;
   // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
   // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
   const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
+  const bool force_to = a.flags & kFlagForceTimeout;
   R* xsave = static_cast<R*>(a.x_save);
   const int TTf = (int)T + B.dmax;
   const R* q0p = static_cast<const R*>(a.q0);
@@ -247,7 +290,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   load_math_tables();
   __syncthreads();
   unsigned long long prof_wait = 0;
-  if (a.prof && tid == 0) prof_begin(a.prof);
+  if (a.prof && tid == 0) prof_begin(a.prof, bid);
 
   // q'[max(t-1,0)] * flow_scale (gathered into the schedule layout: one row per tick), or the
   // carried Q0 at t = 0, for the step each reach runs at tick `tau`
@@ -282,7 +325,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int e = a.s.v_edge[B.virt0 + v];
         const int t = tau + sidx - a.s.v_off[B.virt0 + v];
         double val = 0.0;
-        if (t >= 0 && t < T) val = wait_granule(a.bnd + (int64_t)e * T + t, a.status);
+        if (t >= 0 && t < T) val = wait_granule(a.bnd + (int64_t)e * T + t, a.status, blockIdx.x, force_to);
         ring[v * kChunk + sidx] = val;
       }
       lds_barrier();
@@ -349,14 +392,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         xk[k] = x;
         if (hk && t >= 0 && t < T) {
           const R xr = R(x);
-          const R Qn = raw ? xr : rmax(xr, cs.qlb);
+          const R Qn = raw ? xr : rmax_nan(xr, cs.qlb);
           xrow[r] = xr;  // the routing state for the adjoint
           if (emit) {
             // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
             ob0[k] = ob1[k];
             ob1[k] = ob2[k];
             ob2[k] = ob3[k];
-            ob3[k] = rmax(xr, cs.qlb);
+            ob3[k] = rmax_nan(xr, cs.qlb);
             R* orow = runoff + (int64_t)ref[k] * T;
             if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
@@ -396,60 +439,85 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
 #pragma unroll 1
   for (int tau = 0; tau < TT; ++tau) {
-    if (a.prof && tid == 0) prof_tick(a.prof, tau);
+    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
     tick(tau, qa, qb);
 #pragma unroll
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
-  if (a.prof && tid == 0) prof_end(a.prof, prof_wait);
+  if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
 }
+
+template <typename R>
+struct Grad4 {
+  R a, b, c, d;
+};
+template <typename R>
+__device__ __forceinline__ Grad4<R> make_grad4(R a, R b, R c, R d) { return Grad4<R>{a, b, c, d}; }
 
 // ============================================================================================
 // Backward (adjoint)
 // ============================================================================================
-// Reverse ticks; per tick:
+// Reverse ticks (backward tick tb runs forward tick tau = TT - 1 - tb: reach i at step
+// t = tau - off(i), its upstream reaches at t + 1, its downstream at t - 1); per tick:
 //   [import a chunk of (c1 gb, c2 gb) from downstream blocks]
-//   read:    the downstream reach's (c1_d gb_d, c2_d gb_d) from its slot (or the ring); export the
-//            consumers' values of virtual inflows to the upstream blocks            -- barrier --
-//   compute: VJP of one step, own slot <- (c1 gb, c2 gb)                             -- barrier --
+//   read:    publish x(t - 2) of every reach (and of every virtual inflow, from the forward's
+//            boundary granules) into its slot; read the downstream reach's (c1_d gb_d, c2_d gb_d)
+//            from its slot (or the ring); export the consumers' values of virtual inflows to the
+//            upstream blocks                                                          -- barrier --
+//   compute: from the upstream slots x_j(t - 1): the inflow I(t) of this step and the upstream sum
+//            Sx(t - 1) of the next one (Sx(t) was formed last tick); VJP of one step; own slot
+//            <- (c1 gb, c2 gb)                                                         -- barrier --
+// Every global load of a tick is issued one tick (own states: two ticks) before its use: the
+// states x(t - 3) (the schedule layout, coalesced rows), the virtual inflows' x, and dL/drunoff read
+// straight from the API's (N, T) layout in 16-B groups of four steps (gauge mode: summed over the
+// reach's gauges from (G, T)).
 template <typename R, int KR>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
-  const BlockDesc B = a.s.blocks[blockIdx.x];
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int bid = take_ticket(a.status, kStatusTicketBwd, a.nblocks, true, reinterpret_cast<int*>(smem));
+  const BlockDesc B = block_desc(a.s.blocks, bid);
   const int tid = threadIdx.x;
   // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
   // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* sa = reinterpret_cast<double*>(smem + kMathTabBytes);  // [S] c1_i * gb_i  (fp64, transposed solve)
-  R* sb = reinterpret_cast<R*>(sa + S);                           // [S] c2_i * gb_i
-  const StatTab<R> tab{sb + S};                                   // [S][6]
-  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 7 * sizeof(R))));  // [ncout][kChunk][2]
+  R* sa = reinterpret_cast<R*>(smem + kMathTabBytes);  // [S] c1_i gb_i (transposed solve, rounded to R)
+  R* sb = sa + S;                                       // [S] c2_i gb_i (adjoint of the inflow)
+  R* sx = sb + S;                                       // [S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
+  const StatTab<R> tab{sx + S};                         // [S][6]
+  R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * 9 * sizeof(R)));  // [ncout][kChunk][2]
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
+  const bool force_to = a.flags & kFlagForceTimeout;
   const R* xsave = static_cast<const R*>(a.x_save);
-  const R* gsch = static_cast<const R*>(a.gs);
+  const R* gout = static_cast<const R*>(a.grad_out);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
+  const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
 
-  int ref[KR], off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
+  // ref (the reference reach id) is re-read from the schedule where it is needed (every fourth
+  // step and every kGradFlush steps) rather than held in a register
+  int off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
   unsigned up[KR];
-  R lam[KR], xc[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR];  // xc = x(t), xa = x(t-1), xb = x(t-2) prefetch
+  // xc = x(t), xa = x(t-1), xb = x(t-2) (published this tick, then reloaded with x(t-3), while
+  // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
+  // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
+  R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
-    ref[k] = a.s.ref[P];
     off[k] = a.s.off[P];
     dl[k] = a.s.dloc[P];
-    up[k] = pack_up(a, P);
-    lam[k] = R(0);
+    up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
+    lam[k] = sxn[k] = R(0);
     xc[k] = xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
-    if (hk) tab.put(r, load_static<R>(a, ref[k]));
+    g0[k] = g1[k] = g2[k] = g3[k] = R(0);
+    if (hk) tab.put(r, load_static<R>(a, a.s.ref[P]));
   }
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
@@ -457,7 +525,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k)
       if (tid + k * BS == loc) dl[k] = -(c + 2);
   }
-  const R* qsb = static_cast<const R*>(a.qs) + xs_base;  // q' * flow_scale, schedule layout
+  if (tid == 0) sx[S - 1] = R(0);
   const bool vown = tid < B.nvirt;
   int v_edge = 0, v_off = 0, v_dloc = 0;
   if (vown) {
@@ -469,7 +537,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   load_math_tables();
   __syncthreads();
   unsigned long long prof_wait = 0;
-  if (a.prof && tid == 0) prof_begin(a.prof);
+  if (a.prof && tid == 0) prof_begin(a.prof, bid);
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
   auto load_own = [&](int tau, R(&dst)[KR], int tq) {
@@ -481,26 +549,48 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       dst[k] = xsave[xs_base + (int64_t)tc * B.nloc + (r < B.nloc ? r : 0)];
     }
   };
-  // x of upstream slot u at step t: a reach of this block (row of its tick, one load at a scalar
-  // base), or a virtual inflow (the forward's boundary granule)
-  auto up_x = [&](int u, const R* row, int64_t t) -> R {
-    if (u < B.nloc) return row[u];
-    const int e = a.s.v_edge[B.virt0 + (u - B.nloc)];
-    const int64_t tt = t < 0 ? 0 : t;
-    return R(a.bnd[(int64_t)e * T + tt]);
+  // x of a virtual inflow (the upstream reach of cut edge v_edge) at step t, from the forward's
+  // boundary granules (t clamped into [0, T))
+  auto load_virt = [&](int64_t t) -> R {
+    const int64_t tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
+    return R(a.bnd[(int64_t)v_edge * T + tc]);
+  };
+  // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
+  // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439)
+  auto load_grad = [&](int ref, int64_t base) {
+    R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
+    const int64_t i1 = base + 1 < T ? base + 1 : T - 1, i2 = base + 2 < T ? base + 2 : T - 1,
+                  i3 = base + 3 < T ? base + 3 : T - 1;
+    auto add_row = [&](const R* row) {
+      if (vec4) {
+        if constexpr (sizeof(R) == 4) {
+          const float4 v = *reinterpret_cast<const float4*>(row + base);
+          v0 = v0 + v.x; v1 = v1 + v.y; v2 = v2 + v.z; v3 = v3 + v.w;
+        } else {
+          const double2 u = reinterpret_cast<const double2*>(row + base)[0];
+          const double2 w = reinterpret_cast<const double2*>(row + base)[1];
+          v0 = v0 + u.x; v1 = v1 + u.y; v2 = v2 + w.x; v3 = v3 + w.y;
+        }
+      } else {
+        v0 = v0 + row[base]; v1 = v1 + row[i1]; v2 = v2 + row[i2]; v3 = v3 + row[i3];
+      }
+    };
+    if (a.g_roff) {
+      const int64_t q1 = a.g_roff[ref + 1];
+      for (int64_t q = a.g_roff[ref]; q < q1; ++q) add_row(gout + a.g_rg[q] * T);
+    } else {
+      add_row(gout + (int64_t)ref * T);
+    }
+    return make_grad4(v0, v1, v2, v3);
   };
 
-  // xp = x(t-1) of the step each reach runs at this tick; xn receives x(t-2) for the next tick
-  auto tick = [&](int tb, R(&xp)[KR], R(&xn)[KR]) {
+  R vx = R(0);  // virtual inflow's x(t_v - 2), prefetched one tick ahead
+
+  auto tick = [&](int tb) {
     const int tau = TT - 1 - tb;  // forward tick
-    const R* xrow1 = xsave + xs_base + (int64_t)(tau >= 1 ? tau - 1 : 0) * B.nloc;  // x(t-1) of this block
-    const R* xrow2 = xsave + xs_base + (int64_t)(tau >= 2 ? tau - 2 : 0) * B.nloc;  // x(t-2)
-    const R* grow = gsch + xs_base + (int64_t)tau * B.nloc;
-    const R* qrow = qsb + (int64_t)tau * B.nloc;
     const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      ref[k] = opq(ref[k]);
       off[k] = opq(off[k]);
       up[k] = opq(up[k]);
       dl[k] = opq(dl[k]);
@@ -512,10 +602,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int P = B.pos0 + a.s.cout_loc[B.cout0 + c];
         const int e = a.s.cut[P];
         const int t = (tau - sidx) - a.s.off[P];
-        double A = 0.0, Bv = 0.0;
+        R A = R(0), Bv = R(0);
         if (t >= 1 && t < T) {
-          A = wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2, a.status);
-          Bv = wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2 + 1, a.status);
+          A = R(wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2, a.status, bid, force_to));
+          Bv = R(wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2 + 1, a.status, bid, force_to));
         }
         ring[(c * kChunk + sidx) * 2] = A;
         ring[(c * kChunk + sidx) * 2 + 1] = Bv;
@@ -523,35 +613,39 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
-    // ---- read ---------------------------------------------------------------------------------
+    // ---- read / publish ----------------------------------------------------------------------
     if (vown) {
-      // export the consumer's (c1 gb, c2 gb) of step t to the upstream block
+      // export the consumer's (c1 gb, c2 gb) of step t (written last tick, when the consumer ran
+      // step tau + 1 - off_c = tau - v_off) to the upstream block; publish the upstream reach's x
+      // at the consumer's current step - 1
       const int t = tau - v_off;
       if (t >= 1 && t < T) {
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, sa[v_dloc]);
+        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[v_dloc]);
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[v_dloc]);
       }
+      sx[B.nloc + tid] = vx;
     }
-    double A[KR];
-    R Bd[KR];
+    R A[KR], Bd[KR];
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      A[k] = 0.0;
+      A[k] = R(0);
       Bd[k] = R(0);
       if (wbase + k * BS >= B.nloc) continue;
+      const int r = tq + k * BS;
+      if (r < B.nloc) sx[r] = xb[k];  // x(t - 2): the upstream value of the downstream reach's step t - 1
       if (dl[k] >= 0) {
         A[k] = sa[dl[k]];
         Bd[k] = sb[dl[k]];
       } else if (dl[k] <= -2) {
         const int sidx = tb % kChunk;
         A[k] = ring[((-dl[k] - 2) * kChunk + sidx) * 2];
-        Bd[k] = R(ring[((-dl[k] - 2) * kChunk + sidx) * 2 + 1]);
+        Bd[k] = ring[((-dl[k] - 2) * kChunk + sidx) * 2 + 1];
       }
     }
     lds_barrier();
-    load_own(tau - 2, xn, tq);  // for the next tick
-    // ---- compute (one reach at a time; its loads are issued first and consumed after the
-    //      geometry recompute, which hides their latency) ------------------------------------
+    load_own(tau - 3, xb, tq);                    // x(t - 3), published next tick
+    if (vown) vx = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
+    // ---- compute ------------------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       if (wbase + k * BS >= B.nloc) continue;
@@ -560,42 +654,43 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int rs = hk ? r : 0;
       const int t = tau - off[k];
       const bool active = hk && t >= 1 && t < T;
-      const int64_t tcl = t < 0 ? 0 : (t >= T ? T - 1 : t);
-      const R xtk = xc[k];                 // own x(t) (kept from the previous tick)
-      const R gk = grow[rs];               // dL/dQ_t (expand_grad_kernel)
-      const R qvk = qrow[rs];              // q'[t-1] * flow_scale (mmc.py:303-304)
-      const R xu0 = up_x(up_0(up[k]), xrow1, tcl);
-      const R xu1 = up_x(up_1(up[k]), xrow1, tcl);
-      const R xup0 = up_x(up_0(up[k]), xrow2, tcl - 1);
-      const R xup1 = up_x(up_1(up[k]), xrow2, tcl - 1);
-      const ReachStatic<R> st = tab.template get<true>(rs);
-      const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
-      const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
-      const double gb64 = (double)gx + A[k];             // (I - C1 N)^T gb = gx in fp64 (utils.py:188-242)
-      const R gb = R(gb64);
-      const R Qp = (t == 1 && carry) ? xp[k] : rmax(xp[k], cs.qlb);
-      const int nup = up_n(up[k]);
-      R Sx = R(0), I = R(0);
+      // upstream x_j(t - 1): I(t) = sum_j Q_j(t - 1) (mmc.py:535, ascending columns; the carried
+      // state at t - 1 = 0 is not clamped) and Sx(t - 1) for the next tick
       const bool c0 = (t == 1 && carry);
-      Sx = Sx + (nup > 0 ? xu0 : R(0));
-      Sx = Sx + (nup > 1 ? xu1 : R(0));
-      I = I + (nup > 0 ? (c0 ? xup0 : rmax(xup0, cs.qlb)) : R(0));
-      I = I + (nup > 1 ? (c0 ? xup1 : rmax(xup1, cs.qlb)) : R(0));
+      const int nup = up_n(up[k]);
+      const R x0 = sx[up_0(up[k])];
+      const R x1 = sx[up_1(up[k])];
+      R sxv = R(0) + x0;
+      sxv = sxv + x1;
+      R I = R(0);
+      I = I + (nup > 0 ? (c0 ? x0 : rmax(x0, cs.qlb)) : R(0));
+      I = I + (nup > 1 ? (c0 ? x1 : rmax(x1, cs.qlb)) : R(0));
       if (nup > 2) {
         const int P = B.pos0 + r;
-        const int b = a.s.upb[P], c = a.s.upc[P];
+        const int bb = a.s.upb[P], c = a.s.upc[P];
         for (int j = 2; j < c; ++j) {
-          const int u = a.s.uplist[b + j];
-          Sx = Sx + up_x(u, xrow1, t);
-          const R xj = up_x(u, xrow2, t - 1);
+          const R xj = sx[a.s.uplist[bb + j]];
+          sxv = sxv + xj;
           I = I + (c0 ? xj : rmax(xj, cs.qlb));
         }
       }
+      const R Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
+      sxn[k] = sxv;
+      const int e4 = t & 3;
+      const R gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+      const R xtk = xc[k];
+      const ReachStatic<R> st = tab.template get<true>(rs);
+      const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
+      const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
+      const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
+      const R gb = R(gb64);
+      const R Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);     // Q_{t-1}
       R c1, c2, c3, gQ, gn, gq, gp;
       if constexpr (std::is_same<R, float>::value) {
         const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
         c1 = o.c1; c2 = o.c2; c3 = o.c3; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
       } else {
+        const R qvk = static_cast<const R*>(a.qs)[xs_base + (int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale
         R c4, tw, ss;
         Geom<R> geo;
         coefficients<R, true>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
@@ -611,35 +706,73 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         // t, not to ticks, so the summation grouping -- and the result -- is independent of the
         // partition); one owner per address, so the atomics are deterministic
         if ((t % kGradFlush) == 1 || t == 1) {
-          double* g3 = gacc + (int64_t)ref[k] * 3;
-          atomicAdd(g3 + 0, (double)pn[k]);
-          atomicAdd(g3 + 1, (double)pq[k]);
-          atomicAdd(g3 + 2, (double)pp[k]);
+          double* g3p = gacc + (int64_t)a.s.ref[B.pos0 + r] * 3;
+          atomicAdd(g3p + 0, (double)pn[k]);
+          atomicAdd(g3p + 1, (double)pq[k]);
+          atomicAdd(g3p + 2, (double)pp[k]);
           pn[k] = pq[k] = pp[k] = R(0);
         }
-        sa[r] = (double)c1 * gb64;
+        sa[r] = R((double)c1 * gb64);
         sb[r] = c2 * gb;
         lam[k] = ((gb * c3) + gQ) + Bd[k];
+      }
+      // dL/drunoff of the next step's group, one tick ahead
+      const int tn = t - 1;
+      if (hk && tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)) {
+        const Grad4<R> v = load_grad(a.s.ref[B.pos0 + r], (int64_t)(tn & ~3));
+        g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     lds_barrier();
-  };
-
-  // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2
-  load_own(TT - 1, xc, tid);
-  load_own(TT - 2, xa, tid);
-#pragma unroll 1
-  for (int tb = 0; tb < TT; ++tb) {
-    if (a.prof && tid == 0) prof_tick(a.prof, tb);
-    tick(tb, xa, xb);
+    // next tick: x(t - 1) -> x(t); x(t - 2), still in the own slot -> x(t - 1)
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
+      const int r = tq + k * BS;
       xc[k] = xa[k];
-      xa[k] = xb[k];
+      xa[k] = r < B.nloc ? sx[r] : R(0);
     }
+  };
+
+  // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2, x(t-2) at row TT-3
+  load_own(TT - 1, xc, tid);
+  load_own(TT - 2, xa, tid);
+  load_own(TT - 3, xb, tid);
+  // prologue: Sx of every reach's first step t0 = sum_j x_j(t0), where x_j(t0) is the upstream
+  // reach's x one step before its own first step (its xa; a virtual inflow's granule)
+#pragma unroll
+  for (int k = 0; k < KR; ++k)
+    if (tid + k * BS < B.nloc) sx[tid + k * BS] = xa[k];
+  if (vown) sx[B.nloc + tid] = load_virt((int64_t)(TT - 1) - v_off - 1);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KR; ++k) {
+    const int r = tid + k * BS;
+    if (r >= B.nloc) continue;
+    R v = R(0) + sx[up_0(up[k])];
+    v = v + sx[up_1(up[k])];
+    if (up_n(up[k]) > 2) {
+      const int P = B.pos0 + r;
+      const int bb = a.s.upb[P], c = a.s.upc[P];
+      for (int j = 2; j < c; ++j) v = v + sx[a.s.uplist[bb + j]];
+    }
+    sxn[k] = v;
   }
-  if (a.prof && tid == 0) prof_end(a.prof, prof_wait);
+  __syncthreads();
+  if (vown) vx = load_virt((int64_t)(TT - 1) - v_off - 2);
+#pragma unroll
+  for (int k = 0; k < KR; ++k)
+    if (tid + k * BS < B.nloc && TT - 1 - off[k] == T - 1) {
+      const Grad4<R> v = load_grad(a.s.ref[B.pos0 + tid + k * BS], (T - 1) & ~int64_t(3));
+      g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
+    }
+#pragma unroll 1
+  for (int tb = 0; tb < TT; ++tb) {
+    if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+    tick(tb);
+  }
+  if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
 }
 
 // Final fp64 accumulators -> R gradients (reference order).
@@ -653,10 +786,9 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
 }
 
 // ============================================================================================
-// Layout transposes between the API's (reach, step) arrays and the schedule layout of x_save
-// (per workgroup, tick-major: row tau = t + off(r) holds its nloc reaches contiguously).  Each
-// thread issues all its loads before the first is consumed (memory-level parallelism); the tile's
-// reference ids are staged in LDS so the scattered side has no dependent global loads.
+// Lateral inflow into the schedule layout of x_save (per workgroup, tick-major: row tau = t + off(r)
+// holds its nloc reaches contiguously).  Each thread issues all its loads before the first is
+// consumed (memory-level parallelism).
 // ============================================================================================
 
 // q'[max(t-1, 0), ref] * flow_scale[ref] -> qs[tick(t, r)] (mmc.py:303-304, 421-424): the routing
@@ -710,110 +842,6 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   }
 }
 
-// Tiles of kTileR reaches x TrSteps<R> steps, 1024 threads, 16 elements per thread: the (reach,
-// step) side moves whole rows of TrSteps steps per reach (1 KiB), the schedule side runs of
-// positions of one tick offset; the tile (~66 KiB) is staged in LDS.
-#ifndef DDR_TR_ROW
-#define DDR_TR_ROW 256
-#endif
-#ifndef DDR_TR_THREADS
-#define DDR_TR_THREADS 1024
-#endif
-template <typename R>
-constexpr int TrSteps = DDR_TR_ROW / sizeof(R);
-constexpr int kTrThreads = DDR_TR_THREADS;
-
-// runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
-template <typename R>
-__global__ void __launch_bounds__(kTrThreads) emit_runoff_kernel(RouteArgs a) {
-  constexpr int TS = TrSteps<R>, PER = kTileR * TS / kTrThreads;
-  constexpr int RS = kTrThreads / kTileR, TSS = kTrThreads / TS;  // row strides of the two phases
-  __shared__ R tile[TS][kTileR + 1];
-  __shared__ int sref[kTileR];
-  const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
-  const BlockDesc B = a.s.blocks[b];
-  const int nr = min(kTileR, B.nloc - r0);
-  const int64_t T = a.T;
-  const int64_t t0 = (int64_t)blockIdx.y * TS;
-  const R* xs = static_cast<const R*>(a.x_save) + T * B.pos0 + B.pre_dn;
-  R* out = static_cast<R*>(a.runoff);
-  const R qlb = R(a.c[1]);
-  const int tid = threadIdx.x;
-  if (tid < kTileR) sref[tid] = a.s.ref[B.pos0 + r0 + (tid < nr ? tid : 0)];
-  {
-    const int i = tid % kTileR, j0 = tid / kTileR;  // reach fastest: coalesced along a tick row
-    const int ic = i < nr ? i : 0;
-    const int off = a.s.off[B.pos0 + r0 + ic];
-    R v[PER];
-#pragma unroll
-    for (int m = 0; m < PER; ++m) {
-      int64_t t = t0 + j0 + RS * m;
-      t = t < T ? t : T - 1;
-      v[m] = xs[(t + off) * B.nloc + r0 + ic];
-    }
-#pragma unroll
-    for (int m = 0; m < PER; ++m) tile[j0 + RS * m][i] = v[m];
-  }
-  __syncthreads();
-  const int j = tid % TS, i0 = tid / TS;  // step fastest: coalesced along a reach row
-  if (t0 + j < T) {
-#pragma unroll
-    for (int m = 0; m < PER; ++m) {
-      const int i = i0 + TSS * m;
-      if (i < nr) out[(int64_t)sref[i] * T + t0 + j] = rmax(tile[j][i], qlb);
-    }
-  }
-}
-
-// gs[tick(t, r)] = dL/drunoff[ref(r), t], or in gauge mode sum over the reach's gauges g of
-// dL/dout[g, t] (mmc.py:405-411: every gauge sums the clamped discharge of its reaches)
-template <typename R>
-__global__ void __launch_bounds__(kTrThreads) expand_grad_kernel(RouteArgs a) {
-  constexpr int TS = TrSteps<R>, PER = kTileR * TS / kTrThreads;
-  constexpr int RS = kTrThreads / kTileR, TSS = kTrThreads / TS;
-  __shared__ R tile[TS][kTileR + 1];
-  __shared__ int sref[kTileR];
-  const int b = a.s.rtile[2 * blockIdx.x], r0 = a.s.rtile[2 * blockIdx.x + 1];
-  const BlockDesc B = a.s.blocks[b];
-  const int nr = min(kTileR, B.nloc - r0);
-  const int64_t T = a.T;
-  const int64_t t0 = (int64_t)blockIdx.y * TS;
-  const R* go = static_cast<const R*>(a.grad_out);
-  R* gs = static_cast<R*>(a.gs) + T * B.pos0 + B.pre_dn;
-  const int tid = threadIdx.x;
-  if (tid < kTileR) sref[tid] = a.s.ref[B.pos0 + r0 + (tid < nr ? tid : 0)];
-  __syncthreads();
-  {
-    const int j = tid % TS, i0 = tid / TS;  // step fastest: coalesced along a reach row
-    const int64_t tc = t0 + j < T ? t0 + j : T - 1;
-    R v[PER];
-    if (a.g_roff) {
-#pragma unroll
-      for (int m = 0; m < PER; ++m) {
-        const int64_t ref = sref[i0 + TSS * m];
-        R g = R(0);
-        for (int64_t q = a.g_roff[ref]; q < a.g_roff[ref + 1]; ++q) g = g + go[a.g_rg[q] * T + tc];
-        v[m] = g;
-      }
-    } else {
-#pragma unroll
-      for (int m = 0; m < PER; ++m) v[m] = go[(int64_t)sref[i0 + TSS * m] * T + tc];
-    }
-#pragma unroll
-    for (int m = 0; m < PER; ++m) tile[j][i0 + TSS * m] = v[m];
-  }
-  __syncthreads();
-  const int i = tid % kTileR, j0 = tid / kTileR;  // reach fastest: coalesced along a tick row
-  if (i < nr) {
-    const int off = a.s.off[B.pos0 + r0 + i];
-#pragma unroll
-    for (int m = 0; m < PER; ++m) {
-      const int64_t t = t0 + j0 + RS * m;
-      if (t < T) gs[(t + off) * B.nloc + r0 + i] = tile[j0 + RS * m][i];
-    }
-  }
-}
-
 // ============================================================================================
 // Gauge reduction: out[g, t] = sum_{k} clamp(x_t[idx_k])  (mmc.py:405-411, 433-439)
 // ============================================================================================
@@ -829,11 +857,11 @@ __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
     const int r = P - B.pos0;
     const int64_t tick = t + a.s.off[P];
     const R x = xsave[a.T * B.pos0 + B.pre_dn + tick * B.nloc + r];
-    const R Q = (t == 0 && a.carry) ? x : rmax(x, R(a.qlb));
+    const R Q = (t == 0 && a.carry) ? x : rmax_nan(x, R(a.qlb));
     acc = acc + Q;
   }
   // output[:, 0] = clamp(initial) (mmc.py:412); later steps are sums of clamped states
-  out[g * a.T + t] = (t == 0) ? rmax(acc, R(a.qlb)) : acc;
+  out[g * a.T + t] = (t == 0) ? rmax_nan(acc, R(a.qlb)) : acc;
 }
 
 // ============================================================================================
@@ -848,8 +876,8 @@ template <typename R, int KR>
 hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream_t stream) {
   const size_t smem = route_smem_bytes<R>(g, backward);
   a.slot_stride = route_slot_stride(g->max_slots);
-  a.ring_stride = backward ? 2 * kChunk : kChunk;
   a.n_cut = g->n_cut;
+  a.nblocks = (int32_t)g->blocks.size();
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
     auto kern = route_backward_kernel<R, KR>;
@@ -896,35 +924,18 @@ int max_resident_blocks(const Graph* g, bool backward) {
 }
 
 template <typename R>
-hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream) {
-  if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
-  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + TrSteps<R> - 1) / TrSteps<R>));
-  hipLaunchKernelGGL(emit_runoff_kernel<R>, grid, dim3(kTrThreads), 0, stream, a);
-  return hipGetLastError();
-}
-
-template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream) {
   if (g->max_nloc == 0 || a.T == 0) return hipSuccess;
 #ifndef DDR_GATHER_G
 #define DDR_GATHER_G 8
 #endif
   constexpr int G = sizeof(R) == 4 ? DDR_GATHER_G : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
-  a.gather_steps = G;
   const size_t smem = (size_t)G * g->max_nloc * sizeof(R);
   auto kern = gather_qprime_kernel<R, G>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + G - 1) / G));
   hipLaunchKernelGGL(kern, grid, dim3(1024), smem, stream, a);
-  return hipGetLastError();
-}
-
-template <typename R>
-hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream) {
-  if (g->n_rtiles == 0 || a.T == 0) return hipSuccess;
-  const dim3 grid((unsigned)g->n_rtiles, (unsigned)((a.T + TrSteps<R> - 1) / TrSteps<R>));
-  hipLaunchKernelGGL(expand_grad_kernel<R>, grid, dim3(kTrThreads), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -942,12 +953,8 @@ template hipError_t launch_route<float>(const Graph*, const RouteArgs&, bool, hi
 template hipError_t launch_route<double>(const Graph*, const RouteArgs&, bool, hipStream_t);
 template int max_resident_blocks<float>(const Graph*, bool);
 template int max_resident_blocks<double>(const Graph*, bool);
-template hipError_t launch_emit_runoff<float>(const Graph*, const RouteArgs&, hipStream_t);
-template hipError_t launch_emit_runoff<double>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_gather_qprime<float>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_gather_qprime<double>(const Graph*, RouteArgs&, hipStream_t);
-template hipError_t launch_expand_grad<float>(const Graph*, const RouteArgs&, hipStream_t);
-template hipError_t launch_expand_grad<double>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_gauge<float>(const GaugeArgs&, const float*, float*, hipStream_t);
 template hipError_t launch_gauge<double>(const GaugeArgs&, const double*, double*, hipStream_t);
 

@@ -11,7 +11,7 @@ struct RouteArgs {
   int64_t n_cut;
   int32_t flags;
   int32_t slot_stride;  // LDS slots per buffer (max nloc + nvirt over blocks)
-  int32_t ring_stride;  // doubles per virtual/cut-out import ring
+  int32_t nblocks;      // logical blocks (tickets) of a routing launch
   int32_t p_stride;
   const void* n;
   const void* q;
@@ -25,15 +25,13 @@ struct RouteArgs {
   void* runoff;
   void* x_save;
   void* qs;              // lateral inflow in the schedule layout (second half of the x_save workspace)
-  int32_t gather_steps;  // steps per gather_qprime_kernel tile
   double* bnd;
   unsigned* status;
   void* q_last;
   void* tw_last;
   void* ss_last;
   // backward
-  const void* grad_out;
-  void* gs;              // grad_out expanded to the schedule layout of x_save (backward workspace)
+  const void* grad_out;   // dL/drunoff, (N, T) or (G, T) in gauge mode
   const int64_t* g_roff;
   const int64_t* g_rg;
   double* bwd_bnd;
@@ -63,11 +61,7 @@ hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipSt
 template <typename R>
 int max_resident_blocks(const Graph* g, bool backward);
 template <typename R>
-hipError_t launch_emit_runoff(const Graph* g, const RouteArgs& a, hipStream_t stream);
-template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream);
-template <typename R>
-hipError_t launch_expand_grad(const Graph* g, const RouteArgs& a, hipStream_t stream);
 template <typename R>
 hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t stream);
 

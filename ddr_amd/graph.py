@@ -35,6 +35,7 @@ class GraphInfo:
     bwd_elems_per_t: int
     bwd_elems_fixed: int
     status_bytes: int
+    generations: int
 
 
 def adjacency_to_coo(adj) -> tuple[int, np.ndarray, np.ndarray]:
@@ -52,13 +53,13 @@ def adjacency_to_coo(adj) -> tuple[int, np.ndarray, np.ndarray]:
             col = adj.col_indices().cpu().numpy().astype(np.int64)
             vals = adj.values().detach().cpu().numpy()
             rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(crow))
-            keep = vals != 0
+            keep = _unit_values(vals)
             return n, rows[keep].astype(np.int32), col[keep].astype(np.int32)
         if adj.layout == torch.sparse_coo:
             a = adj.coalesce()
             idx = a.indices().cpu().numpy()
             vals = a.values().detach().cpu().numpy()
-            keep = vals != 0
+            keep = _unit_values(vals)
             return n, idx[0][keep].astype(np.int32), idx[1][keep].astype(np.int32)
         dense = adj.detach().cpu().numpy()
     else:
@@ -67,13 +68,30 @@ def adjacency_to_coo(adj) -> tuple[int, np.ndarray, np.ndarray]:
 
             if sp.issparse(adj):
                 a = adj.tocoo()
-                keep = a.data != 0
+                a.sum_duplicates()
+                keep = _unit_values(a.data)
                 return int(a.shape[0]), a.row[keep].astype(np.int32), a.col[keep].astype(np.int32)
         except ImportError:  # pragma: no cover
             pass
         dense = np.asarray(adj)
     r, c = np.nonzero(dense)
+    _unit_values(dense[r, c])
     return int(dense.shape[0]), r.astype(np.int32), c.astype(np.int32)
+
+
+def _unit_values(vals) -> np.ndarray:
+    """Mask of the stored entries that are edges; every edge must have weight 1.
+
+    The routing kernels sum upstream discharge unweighted (the reference's ``torch.matmul(network,
+    Q)``, ``mmc.py:535``, with the engine's 0/1 adjacency, ``zarr_io.py:7-76``); a weighted adjacency
+    would silently route differently, so it is rejected.
+    """
+    vals = np.asarray(vals)
+    keep = vals != 0
+    if np.any(vals[keep] != 1):
+        raise ValueError("adjacency values must be 0 or 1 (weighted networks are not supported by the "
+                         "fused routing kernels)")
+    return keep
 
 
 class RiverGraph:
@@ -166,10 +184,9 @@ class RiverGraph:
     def bnd_numel(self, T: int) -> int:
         return self.info.bnd_elems_per_t * T
 
-    def bwd_numel(self, T: int, itemsize: int = 4) -> int:
-        """Backward workspace in doubles: boundary + accumulators, then the gradient expanded to
-        the x_save layout in reals of ``itemsize`` bytes."""
-        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed + -(-self.state_numel(T) * itemsize // 8)
+    def bwd_numel(self, T: int) -> int:
+        """Backward workspace in doubles: cut-edge boundary granules + fp64 gradient accumulators."""
+        return self.info.bwd_elems_per_t * T + self.info.bwd_elems_fixed
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:
@@ -185,4 +202,4 @@ class RiverGraph:
     def __repr__(self) -> str:
         i = self.info
         return (f"RiverGraph(n={i.n}, edges={i.nnz}, basins={i.n_basins}, pieces={i.n_pieces}, blocks={i.n_blocks}, "
-                f"cut={i.n_cut}, depth={i.max_depth}, kr={i.reaches_per_thread})")
+                f"cut={i.n_cut}, depth={i.max_depth}, kr={i.reaches_per_thread}, generations={i.generations})")

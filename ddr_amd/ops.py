@@ -74,7 +74,10 @@ def _gauges(G, g_off, g_idx, r_off, r_g) -> _lib.Gauges | None:
                        r_g.data_ptr() if r_g is not None else None)
 
 
-def _check_inputs(qprime, tensors):
+def _check_inputs(qprime, tensors, p=None):
+    """dtype/device/contiguity, and per-reach lengths: the kernels index every per-reach array by
+    reach id, so a short one would be read out of bounds instead of raising (the reference's
+    broadcasting raises a shape error)."""
     if qprime.dim() != 2:
         raise ValueError("streamflow must be (T, N)")
     if not qprime.is_cuda:
@@ -82,9 +85,23 @@ def _check_inputs(qprime, tensors):
     dt = qprime.dtype
     if dt not in (torch.float32, torch.float64):
         raise TypeError("routing supports float32 and float64")
-    for t in tensors:
-        if t is not None and (t.dtype != dt or t.device != qprime.device or not t.is_contiguous()):
+    N = qprime.shape[1]
+    for name, t in tensors:
+        if t is None:
+            continue
+        if t.dtype != dt or t.device != qprime.device or not t.is_contiguous():
             raise ValueError("all routing inputs must share dtype/device and be contiguous")
+        if t.numel() != N:
+            raise ValueError(f"{name} has {t.numel()} elements, the network has {N} reaches")
+    if p is not None and p.numel() not in (1, N):
+        raise ValueError(f"p_spatial has {p.numel()} elements: expected 1 or {N}")
+
+
+def check_status(wait: bool = True) -> None:
+    """Raise ``DDRError(DDR_ERR_TIMEOUT)`` if an earlier routing launch had a timed-out
+    inter-workgroup hand-off (its outputs hold NaN).  Without ``wait`` only launches that have
+    already completed are inspected; every routing call does that implicitly."""
+    _lib.check(_lib.load().ddr_status_check(1 if wait else 0))
 
 
 @torch.library.custom_op("ddrx::mc_route", mutates_args=())
@@ -96,7 +113,10 @@ def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Te
     """Returns (runoff, q_last, top_width_last, side_slope_last, x_save, bnd).
 
     ``r_off``/``r_g`` (reach -> gauge map) are only consumed by the backward."""
-    _check_inputs(qprime, (n, q, p, length, slope, x_storage, flow_scale, q0))
+    _check_inputs(qprime, (("n", n), ("q_spatial", q), ("length", length), ("slope", slope),
+                           ("x_storage", x_storage), ("flow_scale", flow_scale), ("q0", q0)), p)
+    if p.dtype != qprime.dtype or p.device != qprime.device or not p.is_contiguous():
+        raise ValueError("all routing inputs must share dtype/device and be contiguous")
     g = _graph(graph_id)
     T, N = qprime.shape
     if N != g.n:
@@ -127,7 +147,7 @@ def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Te
         _lib.check(red(g.handle, x_save.data_ptr(), T, C.byref(gz), float(consts[1]), int(fflags), runoff.data_ptr(),
                        stream))
     if _CHECK_STATUS:
-        _lib.check(lib.ddr_graph_status(status.data_ptr(), stream))
+        _lib.check(lib.ddr_status_check(1))
     return runoff, q_last, tw, ss, x_save, bnd
 
 
@@ -154,7 +174,9 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
     gn = torch.empty(N, device=dev, dtype=dt)
     gq = torch.empty(N, device=dev, dtype=dt)
     gp = torch.empty(N, device=dev, dtype=dt)
-    bwd_bnd = torch.empty(g.bwd_numel(T, qprime.element_size()), device=dev, dtype=torch.float64)
+    if grad_runoff.shape[1] != T:
+        raise ValueError("runoff gradient must be (N or G, T)")
+    bwd_bnd = torch.empty(g.bwd_numel(T), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
     lib = _lib.load()
     bwd = lib.ddr_mc_backward_f32 if dt == torch.float32 else lib.ddr_mc_backward_f64
@@ -169,7 +191,7 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
                    C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(),
                    status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), int(flags), stream))
     if _CHECK_STATUS:
-        _lib.check(lib.ddr_graph_status(status.data_ptr(), stream))
+        _lib.check(lib.ddr_status_check(1))
     return gn, gq, gp
 
 
@@ -185,6 +207,9 @@ def _setup_context(ctx, inputs, output):
      flags) = inputs
     runoff, q_last, tw, ss, x_save, bnd = output
     ctx.graph_id = graph_id
+    # strong reference: the registry is weak, and the saved x_save / bnd layouts belong to this
+    # graph's schedule, so it must outlive the backward (a reused id() would pick another graph)
+    ctx.graph = _graph(graph_id)
     ctx.consts = consts
     ctx.flags = flags
     ctx.gauge = g_off is not None

@@ -73,9 +73,11 @@ typedef struct {
   int64_t save_elems_per_t;   /* x_save elements = save_elems_per_t * T + save_elems_fixed  */
   int64_t save_elems_fixed;
   int64_t bnd_elems_per_t;    /* forward boundary buffer doubles = bnd_elems_per_t * T     */
-  int64_t bwd_elems_per_t;    /* backward workspace = 8 * (bwd_elems_per_t * T + bwd_elems_fixed) */
-  int64_t bwd_elems_fixed;    /*   bytes + sizeof(real) * (x_save elements), 8-byte aligned      */
+  int64_t bwd_elems_per_t;    /* backward workspace doubles = bwd_elems_per_t * T + bwd_elems_fixed */
+  int64_t bwd_elems_fixed;
   int64_t status_bytes;       /* device status word block (zeroed by the library)          */
+  int64_t generations;        /* 1: every workgroup of a launch co-resident (time-pipelined);  */
+                              /* g > 1: blocks exceed the device, they run in ~g waves       */
 } ddr_graph_info;
 
 /* Build from a host COO (rows = downstream reach, cols = upstream reach, int32, E entries), the
@@ -85,6 +87,8 @@ typedef struct {
  * Synchronous (the only host-synchronising call besides ddr_graph_status). */
 ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                            const ddr_build_opts* opts, ddr_graph** out);
+/* Any graph size builds: workgroups take ticket-ordered logical blocks, so a schedule with more
+ * blocks than co-resident workgroups still completes (ddr_graph_info.generations > 1). */
 ddr_status ddr_graph_destroy(ddr_graph* g);
 ddr_status ddr_graph_get_info(const ddr_graph* g, ddr_graph_info* info);
 /* Canonical CSR of the adjacency into host buffers: crow (n+1), col (nnz), int64. */
@@ -134,12 +138,14 @@ typedef struct {
 enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4 };
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
+ * Returns DDR_ERR_TIMEOUT instead of launching when an earlier launch's hand-off timed out
+ * (ddr_status_check). 
  *   qprime     (T, N) lateral inflow, time-major, reference order
  *   q0         (N) carried discharge (DDR_FWD_CARRY) or NULL
  *   runoff     (N, T), or NULL / DDR_FWD_NO_RUNOFF (e.g. gauges: ddr_gauge_reduce afterwards)
  *   x_save     required workspace (save_elems_per_t * T + save_elems_fixed reals): the routed
- *              states, then q' * flow_scale, both in the schedule layout; runoff is emitted from
- *              the states by a tiled transpose; keep it unchanged for ddr_mc_backward
+ *              states, then q' * flow_scale, both in the schedule layout (runoff is written
+ *              by the routing kernel itself); keep it unchanged for ddr_mc_backward
  *   bnd        forward boundary buffer (bnd_elems_per_t * T doubles; may be NULL if n_cut == 0);
  *              must be kept unchanged for ddr_mc_backward
  *   status     device status block (status_bytes)
@@ -180,6 +186,15 @@ ddr_status ddr_gauge_reduce_f64(const ddr_graph* g, const double* x_save, int64_
 /* Synchronise `stream` and read the device status block written by the last launches:
  * returns DDR_OK or DDR_ERR_TIMEOUT. */
 ddr_status ddr_graph_status(const void* status, void* stream);
+/* Hand-off failures without a host sync: every routing launch queues an async copy of its status
+ * words; every entry point returns DDR_ERR_TIMEOUT once a queued copy reports a timed-out hand-off
+ * (whose outputs hold NaN).  wait = 1 blocks until every queued copy has landed.  No reference
+ * counterpart (the reference solver raises ValueError on failure, routing/utils.py:598-600). */
+ddr_status ddr_status_check(int32_t wait);
+/* Debug knobs.  DDR_DEBUG_FORCE_TIMEOUT: every inter-workgroup wait of the following launches
+ * times out (tests the failure path). */
+enum { DDR_DEBUG_FORCE_TIMEOUT = 1 };
+ddr_status ddr_set_debug_flags(int32_t flags);
 
 /* General sparse triangular solve A x = b (lower) or A^T x = b (transpose = 1), CSR A with a
  * non-unit diagonal, fp32 values accumulated in fp64 (SciPy semantics, utils.py:587-600).

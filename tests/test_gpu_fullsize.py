@@ -1,4 +1,6 @@
-"""Parity at BASELINE.json's full sizes (C2: 5k reaches x 8760 h; C5: 800k reaches x 8760 h).
+"""Parity at BASELINE.json's full sizes (C2: 5k reaches x 8760 h; C3: 256 gauged subnetworks, 896k
+reaches x 2136 h; C5: 800k reaches x 8760 h; a 1.0M-reach C5-shaped forest that needs two
+generations of workgroups).
 
 The oracle cannot route 800k reaches over a water year in seconds, so the full-size checks use the
 properties the domain offers:
@@ -23,7 +25,7 @@ import torch
 from conftest import maxrel, normrel
 from ddr_amd import synthetic
 from ddr_amd.graph import RiverGraph
-from ddr_amd.ops import RouteConsts, route
+from ddr_amd.ops import GaugeMap, RouteConsts, route
 from ddr_amd.partition import basin_labels, extract_basins
 from oracle import mc_oracle as O
 
@@ -31,6 +33,7 @@ pytestmark = pytest.mark.gpu
 
 RANGES = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
 T_FULL = 8760
+T_C3 = 2136  # rho = 90 days: (90 - 1) * 24 hourly steps (dataclasses.py:115-137, example_config rho 90)
 
 
 def _physical(u):
@@ -157,3 +160,102 @@ def test_c2_full_water_year_matches_oracle(cuda):
     ff = FullForest(net, 2, cuda)
     ref = ff.oracle(np.arange(net.n), grads=False)
     assert maxrel(ff.out["runoff"].cpu().numpy(), ref["runoff"]) <= 1e-6
+
+
+# ---- C3: the training batch of 256 gauged subnetworks ------------------------------------------
+
+
+@pytest.fixture(scope="module")
+def c3(cuda):
+    net = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 3), seed=3, single_inflow=0.25)
+    ff = FullForest(net, 3, cuda, T=T_C3, steps_hint=T_C3)
+    yield ff
+    del ff.qprime, ff.W, ff.out
+    torch.cuda.empty_cache()
+
+
+def test_c3_batch_on_one_gpu_split_basin_matches_oracle(c3):
+    """Round 1 could not build C3 (305 co-resident workgroups needed); it now packs into one resident
+    generation.  The 20k-reach basin is split across workgroups; it matches the oracle with gradients
+    and is bitwise partition invariant (routed alone, it gets a different split)."""
+    info = c3.graph.info
+    assert info.n == 896_201 and info.n_cut > 0
+    assert info.generations == 1 and info.n_blocks <= 256
+    members, nblk = _basins_by_blocks(c3)
+    sizes = np.array([len(m) for m in members])
+    b = int(np.argmax(sizes))
+    assert sizes[b] >= 19_000 and nblk[b] >= 2
+    ids = np.sort(members[b])
+    ref = c3.oracle(ids)
+    sel = torch.from_numpy(ids).to(c3.dev)
+    got = c3.out["runoff"][sel].cpu().numpy()
+    assert maxrel(got, ref["runoff"]) <= 1e-6
+    for k, rk in (("gn", "n"), ("gq", "q_spatial"), ("gp", "p_spatial")):
+        assert normrel(c3.out[k][sel].cpu().numpy(), ref["grads"][rk]) <= 5e-5, k
+    ns, rs, cs = c3.basin(ids)
+    alone = c3.run(RiverGraph(ns, rs, cs, steps_hint=T_C3), ids)
+    np.testing.assert_array_equal(alone["runoff"].cpu().numpy(), got)
+    for k in ("gn", "gq", "gp"):
+        np.testing.assert_array_equal(alone[k].cpu().numpy(), c3.out[k][sel].cpu().numpy())
+
+
+def test_c3_gauge_mode_is_the_outlet_rows(c3):
+    """Gauge mode (one gauge per subnetwork outlet, mmc.py:344-363, 405-411) returns exactly the outlet
+    rows of the full output, and its adjoint equals the full adjoint with dL/drunoff on those rows."""
+    down = c3.net.down
+    outlets = np.flatnonzero(down < 0)
+    assert len(outlets) == 256
+    gz = GaugeMap.build([np.array([o]) for o in outlets], c3.net.n, c3.dev)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(c3.dev)  # noqa: E731
+    sel = torch.from_numpy(outlets).to(c3.dev)
+    Wg = c3.W[sel].contiguous()
+    outs = {}
+    for mode in ("gauge", "masked"):
+        n, q, p = (tt(a).requires_grad_(True) for a in (c3.n, c3.q, c3.p))
+        runoff, _, _, _ = route(c3.graph, c3.qprime, n, q, p, tt(c3.length), tt(c3.slope), tt(c3.x),
+                                gauges=gz if mode == "gauge" else None)
+        if mode == "gauge":
+            runoff.backward(Wg)
+            outs[mode] = (runoff.detach()[:, :], n.grad, q.grad, p.grad)
+        else:
+            Wm = torch.zeros_like(c3.W)
+            Wm[sel] = Wg
+            runoff.backward(Wm)
+            outs[mode] = (runoff.detach()[sel], n.grad, q.grad, p.grad)
+            del Wm
+        torch.cuda.synchronize()
+    for a, b in zip(outs["gauge"], outs["masked"]):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+# ---- beyond one resident generation -----------------------------------------------------------
+
+
+def test_1m_forest_two_generations(cuda):
+    """1.0M reaches (C5-shaped) exceed 256 workgroups of <= 4096 reaches: the schedule packs into two
+    generations of ticket-ordered workgroups and still matches the oracle on sampled basins."""
+    net = synthetic.forest(synthetic.zipf_sizes(1_000_000, 3750, 0.35), seed=6, single_inflow=0.35)
+    ff = FullForest(net, 6, cuda, T=2190)
+    assert ff.graph.info.generations >= 2 and ff.graph.info.n_blocks > 256
+    members, nblk = _basins_by_blocks(ff)
+    sizes = np.array([len(m) for m in members])
+    rng = np.random.default_rng(1)
+    cand = np.flatnonzero((sizes >= 20) & (sizes <= 400))
+    pick = rng.choice(cand, size=4, replace=False)
+    ids = np.sort(np.concatenate([members[i] for i in pick]))
+    ref = ff.oracle(ids)
+    sel = torch.from_numpy(ids).to(cuda)
+    assert maxrel(ff.out["runoff"][sel].cpu().numpy(), ref["runoff"]) <= 1e-6
+    for k, rk in (("gn", "n"), ("gq", "q_spatial"), ("gp", "p_spatial")):
+        assert normrel(ff.out[k][sel].cpu().numpy(), ref["grads"][rk]) <= 5e-5, k
+    multi = [i for i in range(len(members)) if nblk[i] >= 2]
+    b = min(multi, key=lambda i: len(members[i]))
+    ids = np.sort(members[b])
+    ref = ff.oracle(ids, grads=False)
+    assert maxrel(ff.out["runoff"][torch.from_numpy(ids).to(cuda)].cpu().numpy(), ref["runoff"]) <= 1e-6
+    r = ff.out["runoff"]
+    assert bool(torch.isfinite(r).all()) and float(r.min()) >= np.float32(1e-4)
+    for k in ("gn", "gq", "gp"):
+        assert bool(torch.isfinite(ff.out[k]).all()), k
+    del ff.qprime, ff.W, ff.out
+    torch.cuda.empty_cache()

@@ -5,8 +5,7 @@ TAG=${1:-check}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
-export DDR_CHECK_STATUS=1
-timeout -k 10 600 python -u -m pytest $R/tests -v -m gpu -x --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest $R/tests -v -m gpu -x --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?
 grep -E "passed|failed|FAILED|PASSED|^E  " $OUT/pytest.log | cut -c1-300 | head -60
 [ $rc -ne 0 ] && { echo "PYTEST FAILED rc=$rc"; exit $rc; }
