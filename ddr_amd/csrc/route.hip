@@ -104,6 +104,10 @@ __device__ __forceinline__ int take_ticket(unsigned* status, int word, int nbloc
   return bid;
 }
 
+// s_waitcnt vmcnt(0) (expcnt, lgkmcnt unconstrained), gfx9 encoding: an explicit wait the compiler's
+// waitcnt pass sees (inline asm it would not)
+constexpr unsigned kWaitVmcnt0 = 0x0F70;
+
 // Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
 template <typename R>
 __device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a);
@@ -229,6 +233,12 @@ struct StatTab {
 //            physics and the fp64 column sweep, keeps x in a register          -- barrier --
 //   publish: x into the reach's own slot (and virtual inflows into theirs)      -- barrier --
 // The inflow I(t+1) = sum_j Q_j(t) is formed from the same x_j(t) reads (Q_j = clamp(x_j)).
+#ifndef DDR_FWD_TOPWAIT
+#define DDR_FWD_TOPWAIT 1
+#endif
+#ifndef DDR_FWD_UNROLL2
+#define DDR_FWD_UNROLL2 1
+#endif
 template <typename R, int KR>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
@@ -306,6 +316,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR]) {
+#if DDR_FWD_TOPWAIT
+    // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#endif
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
     const int tq = opq(tid);
@@ -436,6 +450,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   const int TT = (int)T + B.dmax;
   prefetch(0, qa, tid);
+#if DDR_FWD_UNROLL2
+  // two ticks per iteration, the prefetch registers swapping roles: copying the prefetched q'
+  // (qa = qb) at the loop latch would wait for the loads just issued, and for every store of the tick
+#pragma unroll 1
+  for (int tau = 0; tau < TT; tau += 2) {
+    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    tick(tau, qa, qb);
+    if (tau + 1 < TT) tick(tau + 1, qb, qa);
+  }
+#else
   // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
 #pragma unroll 1
   for (int tau = 0; tau < TT; ++tau) {
@@ -444,6 +468,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
+#endif
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
 }
 
@@ -497,9 +522,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
   const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
 
-  // ref (the reference reach id) is re-read from the schedule where it is needed (every fourth
-  // step and every kGradFlush steps) rather than held in a register
-  int off[KR], dl[KR];  // dl: local downstream (>= 0), -(import slot + 2), or -1
+  // od packs the tick offset (high 16 bits) and dl (low 16, signed): local downstream (>= 0),
+  // -(import slot + 2), or -1 -- one register for both
+  int ref[KR];
+  unsigned od[KR];
+  auto off_of = [&](int k) { return (int)(od[k] >> 16); };
+  auto dl_of = [&](int k) { return (int)(short)(od[k] & 0xFFFFu); };
   unsigned up[KR];
   // xc = x(t), xa = x(t-1), xb = x(t-2) (published this tick, then reloaded with x(t-3), while
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
@@ -510,20 +538,20 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const int r = tid + k * BS;
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
-    off[k] = a.s.off[P];
-    dl[k] = a.s.dloc[P];
+    ref[k] = a.s.ref[P];
+    od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
     lam[k] = sxn[k] = R(0);
     xc[k] = xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
     g0[k] = g1[k] = g2[k] = g3[k] = R(0);
-    if (hk) tab.put(r, load_static<R>(a, a.s.ref[P]));
+    if (hk) tab.put(r, load_static<R>(a, ref[k]));
   }
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
 #pragma unroll
     for (int k = 0; k < KR; ++k)
-      if (tid + k * BS == loc) dl[k] = -(c + 2);
+      if (tid + k * BS == loc) od[k] = (od[k] & 0xFFFF0000u) | ((unsigned)(-(c + 2)) & 0xFFFFu);
   }
   if (tid == 0) sx[S - 1] = R(0);
   const bool vown = tid < B.nvirt;
@@ -551,9 +579,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
   // x of a virtual inflow (the upstream reach of cut edge v_edge) at step t, from the forward's
   // boundary granules (t clamped into [0, T))
-  auto load_virt = [&](int64_t t) -> R {
+  auto load_virt = [&](int64_t t) -> double {
     const int64_t tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-    return R(a.bnd[(int64_t)v_edge * T + tc]);
+    return a.bnd[(int64_t)v_edge * T + tc];
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
   // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439)
@@ -578,22 +606,40 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if (a.g_roff) {
       const int64_t q1 = a.g_roff[ref + 1];
       for (int64_t q = a.g_roff[ref]; q < q1; ++q) add_row(gout + a.g_rg[q] * T);
-    } else {
-      add_row(gout + (int64_t)ref * T);
+      return make_grad4(v0, v1, v2, v3);
     }
-    return make_grad4(v0, v1, v2, v3);
+    // one reach row: the loaded values as they are (adding them to 0 would consume the load now)
+    const R* row = gout + (int64_t)ref * T;
+    if (vec4) {
+      if constexpr (sizeof(R) == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(row + base);
+        return make_grad4(v.x, v.y, v.z, v.w);
+      } else {
+        const double2 u = reinterpret_cast<const double2*>(row + base)[0];
+        const double2 w = reinterpret_cast<const double2*>(row + base)[1];
+        return make_grad4(u.x, u.y, w.x, w.y);
+      }
+    }
+    return make_grad4(row[base], row[i1], row[i2], row[i3]);
   };
 
-  R vx = R(0);  // virtual inflow's x(t_v - 2), prefetched one tick ahead
+  // virtual inflow's x(t_v - 2), prefetched one tick ahead (kept as loaded: converting it would
+  // wait for the load in the tick that issues it)
+  double vx = 0.0;
 
   auto tick = [&](int tb) {
     const int tau = TT - 1 - tb;  // forward tick
+    // Every global load of the previous tick (states, virtual inflows, gradient groups) lands
+    // here, a whole tick after its issue.  An explicit wait the compiler can see: without it, its
+    // conservative count across the divergent load branches waits (vmcnt(0)) at the first use of a
+    // previous-tick register, i.e. for the loads issued in THIS tick too.
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
-      off[k] = opq(off[k]);
+      ref[k] = opq(ref[k]);
+      od[k] = opq(od[k]);
       up[k] = opq(up[k]);
-      dl[k] = opq(dl[k]);
     }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -623,7 +669,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[v_dloc]);
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[v_dloc]);
       }
-      sx[B.nloc + tid] = vx;
+      sx[B.nloc + tid] = R(vx);
     }
     R A[KR], Bd[KR];
 #pragma unroll
@@ -633,13 +679,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       if (r < B.nloc) sx[r] = xb[k];  // x(t - 2): the upstream value of the downstream reach's step t - 1
-      if (dl[k] >= 0) {
-        A[k] = sa[dl[k]];
-        Bd[k] = sb[dl[k]];
-      } else if (dl[k] <= -2) {
+      const int dl = dl_of(k);
+      if (dl >= 0) {
+        A[k] = sa[dl];
+        Bd[k] = sb[dl];
+      } else if (dl <= -2) {
         const int sidx = tb % kChunk;
-        A[k] = ring[((-dl[k] - 2) * kChunk + sidx) * 2];
-        Bd[k] = ring[((-dl[k] - 2) * kChunk + sidx) * 2 + 1];
+        A[k] = ring[((-dl - 2) * kChunk + sidx) * 2];
+        Bd[k] = ring[((-dl - 2) * kChunk + sidx) * 2 + 1];
       }
     }
     lds_barrier();
@@ -652,7 +699,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int r = tq + k * BS;
       const bool hk = r < B.nloc;
       const int rs = hk ? r : 0;
-      const int t = tau - off[k];
+      const int t = tau - off_of(k);
       const bool active = hk && t >= 1 && t < T;
       // upstream x_j(t - 1): I(t) = sum_j Q_j(t - 1) (mmc.py:535, ascending columns; the carried
       // state at t - 1 = 0 is not clamped) and Sx(t - 1) for the next tick
@@ -706,7 +753,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         // t, not to ticks, so the summation grouping -- and the result -- is independent of the
         // partition); one owner per address, so the atomics are deterministic
         if ((t % kGradFlush) == 1 || t == 1) {
-          double* g3p = gacc + (int64_t)a.s.ref[B.pos0 + r] * 3;
+          double* g3p = gacc + (int64_t)ref[k] * 3;
           atomicAdd(g3p + 0, (double)pn[k]);
           atomicAdd(g3p + 1, (double)pq[k]);
           atomicAdd(g3p + 2, (double)pp[k]);
@@ -719,7 +766,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
       if (hk && tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)) {
-        const Grad4<R> v = load_grad(a.s.ref[B.pos0 + r], (int64_t)(tn & ~3));
+        const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3));
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -744,7 +791,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
   for (int k = 0; k < KR; ++k)
     if (tid + k * BS < B.nloc) sx[tid + k * BS] = xa[k];
-  if (vown) sx[B.nloc + tid] = load_virt((int64_t)(TT - 1) - v_off - 1);
+  if (vown) sx[B.nloc + tid] = R(load_virt((int64_t)(TT - 1) - v_off - 1));
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
@@ -763,8 +810,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if (vown) vx = load_virt((int64_t)(TT - 1) - v_off - 2);
 #pragma unroll
   for (int k = 0; k < KR; ++k)
-    if (tid + k * BS < B.nloc && TT - 1 - off[k] == T - 1) {
-      const Grad4<R> v = load_grad(a.s.ref[B.pos0 + tid + k * BS], (T - 1) & ~int64_t(3));
+    if (tid + k * BS < B.nloc && TT - 1 - off_of(k) == T - 1) {
+      const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3));
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
 #pragma unroll 1
