@@ -35,6 +35,7 @@ DDR_BUILD_HOST_ONLY = 1
 DDR_FWD_SAVE_X = 1
 DDR_FWD_CARRY = 2
 DDR_FWD_NO_RUNOFF = 4
+DDR_FWD_ACCUMULATE = 8
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 
@@ -60,7 +61,7 @@ class Consts(C.Structure):
 class Reaches(C.Structure):
     _fields_ = [("n", C.c_void_p), ("q_spatial", C.c_void_p), ("p_spatial", C.c_void_p), ("p_stride", C.c_int64),
                 ("length", C.c_void_p), ("slope", C.c_void_p), ("x_storage", C.c_void_p),
-                ("flow_scale", C.c_void_p)]
+                ("flow_scale", C.c_void_p), ("qprime_hours", C.c_int64), ("qprime_valid", C.c_void_p)]
 
 
 class Gauges(C.Structure):
@@ -87,6 +88,12 @@ _SIGS = {
                                       C.POINTER(Gauges), _P, _P, _P, _P, _P, _I32, _P]),
     "ddr_gauge_reduce_f32": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _P, _P]),
     "ddr_gauge_reduce_f64": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _P, _P]),
+    "ddr_gauge_daily_f32": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _I64, _I64, _I64, _P, _P]),
+    "ddr_gauge_daily_f64": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _I64, _I64, _I64, _P, _P]),
+    "ddr_gauge_daily_seed_f32": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _P, _P, _P]),
+    "ddr_gauge_daily_seed_f64": (C.c_int, [_I64, _I64, _I64, _I64, _I64, _P, _P, _P]),
+    "ddr_geometry_stats_f32": (C.c_int, [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _P, _P, C.c_double, C.c_double,
+                                         _P, _P]),
     "ddr_graph_status": (C.c_int, [_P, _P]),
     "ddr_status_check": (C.c_int, [_I32]),
     "ddr_set_debug_flags": (C.c_int, [_I32]),

@@ -121,6 +121,7 @@ ddr_status check_common(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   if (!r->n || !r->q_spatial || !r->p_spatial || !r->length || !r->slope || !r->x_storage)
     return fail(DDR_ERR_ARG, "null per-reach input");
   if (r->p_stride != 0 && r->p_stride != 1) return fail(DDR_ERR_ARG, "p_stride must be 0 or 1");
+  if (r->qprime_hours < 0 || r->qprime_hours > (int64_t(1) << 20)) return fail(DDR_ERR_ARG, "bad qprime_hours");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
   if (T * (g->n + 1) > (int64_t(1) << 62)) return fail(DDR_ERR_ARG, "T * N overflows");
   return DDR_OK;
@@ -142,6 +143,9 @@ void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr
   a.S = r->slope;
   a.X = r->x_storage;
   a.fs = r->flow_scale;
+  a.qp_hours = r->qprime_hours > 1 ? (int32_t)r->qprime_hours : 1;
+  a.qp_shift = (flags & DDR_FWD_ACCUMULATE) ? 0 : 1;
+  a.qp_valid = r->qprime_valid;
   a.qprime = qprime;
   a.c[0] = c->dt;
   a.c[1] = c->discharge_lb;
@@ -177,6 +181,8 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   const Graph* g = reinterpret_cast<const Graph*>(gh);
   if (!qprime) return fail(DDR_ERR_ARG, "null qprime");
   if ((flags & DDR_FWD_CARRY) && !q0) return fail(DDR_ERR_ARG, "DDR_FWD_CARRY needs q0");
+  if ((flags & DDR_FWD_CARRY) && (flags & DDR_FWD_ACCUMULATE))
+    return fail(DDR_ERR_ARG, "DDR_FWD_ACCUMULATE has no carried state");
   if (!x_save) return fail(DDR_ERR_ARG, "x_save is required (routing state, and the staging of runoff)");
   if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: bnd buffer required");
   if (!status) return fail(DDR_ERR_ARG, "null status block");
@@ -216,6 +222,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
     return fail(DDR_ERR_ARG, "null backward argument");
   if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: forward boundary buffer required");
   if (!bwd_bnd) return fail(DDR_ERR_ARG, "backward workspace required");
+  if (flags & DDR_FWD_ACCUMULATE) return fail(DDR_ERR_ARG, "DDR_FWD_ACCUMULATE launches have no adjoint");
   if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
     return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
   if ((st = g_pending.check(false))) return st;
@@ -246,12 +253,11 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
 }
 
 template <typename R>
-ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
-                      int32_t flags, R* out, void* stream) {
-  if (!gh || !x_save || !gz || !out || T < 1) return fail(DDR_ERR_ARG, "bad gauge_reduce arguments");
+ddr_status gauge_args(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
+                      int32_t flags, GaugeArgs& a) {
+  if (!gh || !x_save || !gz || T < 1) return fail(DDR_ERR_ARG, "bad gauge arguments");
   if (gz->n_gauges > 0 && (!gz->offsets || !gz->index)) return fail(DDR_ERR_ARG, "null gauge arrays");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
-  GaugeArgs a;
   std::memset(&a, 0, sizeof(a));
   a.s = g->dev;
   a.T = T;
@@ -262,7 +268,45 @@ ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   a.block_of_pos = g->dev.block_of_pos;
   a.qlb = qlb;
   a.carry = (flags & DDR_FWD_CARRY) ? 1 : 0;
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
+                      int32_t flags, R* out, void* stream) {
+  GaugeArgs a;
+  ddr_status st = gauge_args<R>(gh, x_save, T, gz, qlb, flags, a);
+  if (st) return st;
+  if (!out) return fail(DDR_ERR_ARG, "null gauge output");
   DDR_HIP(launch_gauge<R>(a, x_save, out, static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+
+ddr_status check_window(int64_t T, int64_t t0, int64_t L, int64_t D) {
+  if (t0 < 0 || L < 1 || t0 + L > T || D < 1 || D > L)
+    return fail(DDR_ERR_ARG, "daily window must satisfy 0 <= t0, t0 + L <= T, 1 <= D <= L");
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status gauge_daily_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
+                            int32_t flags, int64_t t0, int64_t L, int64_t D, R* out, void* stream) {
+  GaugeArgs a;
+  ddr_status st = gauge_args<R>(gh, x_save, T, gz, qlb, flags, a);
+  if (st) return st;
+  if ((st = check_window(T, t0, L, D))) return st;
+  if (!out) return fail(DDR_ERR_ARG, "null daily output");
+  DDR_HIP(launch_gauge_daily<R>(a, x_save, t0, L, D, out, static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+
+template <typename R>
+ddr_status gauge_daily_seed_impl(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh,
+                                 void* stream) {
+  ddr_status st = check_window(T, t0, L, D);
+  if (st) return st;
+  if (G < 0 || (G > 0 && (!gd || !gh))) return fail(DDR_ERR_ARG, "bad daily seed arguments");
+  DDR_HIP(launch_gauge_daily_seed<R>(G, T, t0, L, D, gd, gh, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
 
@@ -370,6 +414,41 @@ ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t
 ddr_status ddr_gauge_reduce_f64(const ddr_graph* g, const double* x_save, int64_t T, const ddr_gauges* gz,
                                 double qlb, int32_t flags, double* out, void* stream) {
   DDR_GUARD({ return gauge_impl<double>(g, x_save, T, gz, qlb, flags, out, stream); })
+}
+
+ddr_status ddr_gauge_daily_f32(const ddr_graph* g, const float* x_save, int64_t T, const ddr_gauges* gz,
+                               double qlb, int32_t flags, int64_t t0, int64_t L, int64_t D, float* out,
+                               void* stream) {
+  DDR_GUARD({ return gauge_daily_impl<float>(g, x_save, T, gz, qlb, flags, t0, L, D, out, stream); })
+}
+ddr_status ddr_gauge_daily_f64(const ddr_graph* g, const double* x_save, int64_t T, const ddr_gauges* gz,
+                               double qlb, int32_t flags, int64_t t0, int64_t L, int64_t D, double* out,
+                               void* stream) {
+  DDR_GUARD({ return gauge_daily_impl<double>(g, x_save, T, gz, qlb, flags, t0, L, D, out, stream); })
+}
+ddr_status ddr_gauge_daily_seed_f32(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const float* grad_daily,
+                                    float* grad_hourly, void* stream) {
+  DDR_GUARD({ return gauge_daily_seed_impl<float>(G, T, t0, L, D, grad_daily, grad_hourly, stream); })
+}
+ddr_status ddr_gauge_daily_seed_f64(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const double* grad_daily,
+                                    double* grad_hourly, void* stream) {
+  DDR_GUARD({ return gauge_daily_seed_impl<double>(G, T, t0, L, D, grad_daily, grad_hourly, stream); })
+}
+
+ddr_status ddr_geometry_stats_f32(const float* q_daily, int64_t reach_stride, int64_t day_stride, int64_t n,
+                                  int64_t days, const float* n_manning, const float* p_spatial, int64_t p_stride,
+                                  const float* q_spatial, const float* slope, double depth_lb,
+                                  double bottom_width_lb, float* out, void* stream) {
+  DDR_GUARD({
+    if (n < 0 || days < 1 || days > 512) return fail(DDR_ERR_ARG, "geometry statistics: need 1 <= days <= 512");
+    if (n > 0 && (!q_daily || !n_manning || !p_spatial || !q_spatial || !slope || !out))
+      return fail(DDR_ERR_ARG, "null geometry statistics argument");
+    if (p_stride != 0 && p_stride != 1) return fail(DDR_ERR_ARG, "p_stride must be 0 or 1");
+    DDR_HIP(launch_geometry_stats(q_daily, reach_stride, day_stride, n, days, n_manning, p_spatial, p_stride,
+                                  q_spatial, slope, (float)depth_lb, (float)bottom_width_lb, out,
+                                  static_cast<hipStream_t>(stream)));
+    return DDR_OK;
+  })
 }
 
 ddr_status ddr_graph_status(const void* status, void* stream) {

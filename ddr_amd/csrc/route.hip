@@ -260,6 +260,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
+  const bool accum = a.flags & DDR_FWD_ACCUMULATE;  // every step a hot start (daily accumulation)
   const bool force_to = a.flags & kFlagForceTimeout;
   R* xsave = static_cast<R*>(a.x_save);
   const int TTf = (int)T + B.dmax;
@@ -363,7 +364,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         st[h] = tab.get_pre(r < B.nloc ? r : 0, ex[k0 + h], inv[k0 + h]);
         Qv[h] = Q[k0 + h];
       }
-      coefficients_np<R, NP>(st, Qv, cs, ph);
+      if (!accum) {
+        coefficients_np<R, NP>(st, Qv, cs, ph);
+      } else {
+#pragma unroll
+        for (int h = 0; h < NP; ++h) ph[h] = PhysOut<R>{R(0), R(0), R(0), R(0), R(0), R(0)};
+      }
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
         const int k = k0 + h;
@@ -402,7 +408,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             inn = inn + qf(xj);
           }
         }
-        const double x = (t == 0) ? (carry ? (double)qcur[k] : hot) : acc;
+        const double x = (t == 0 && carry) ? (double)qcur[k] : ((t == 0 || accum) ? hot : acc);
         xk[k] = x;
         if (hk && t >= 0 && t < T) {
           const R xr = R(x);
@@ -421,7 +427,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
           if (t == T - 1) {
             if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
-            if (t > 0) {
+            if (t > 0 && !accum) {
               if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = ph[h].tw;
               if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ph[h].ss;
             }
@@ -855,13 +861,18 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   const R* fs = static_cast<const R*>(a.fs);
   const int* rs_loc = a.s.rs_loc + B.pos0;
   const int* rs_ref = a.s.rs_ref + B.pos0;
-  int64_t rowoff[G];  // q' row of step t0 + j: max(t - 1, 0), clamped into [0, T)
+  // q' row of step t = t0 + j (t clamped into [0, T)): max(t - shift, 0) -- step t routes q'[t - 1]
+  // (mmc.py:421-424), shift 0 in accumulation mode -- divided by the hours per stored row (24 for a
+  // daily store: the reader's repeat(24), readers.py:513-519)
+  int64_t rowoff[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     int64_t t = t0 + j;
     t = t < T ? t : T - 1;
-    rowoff[j] = (t > 0 ? t - 1 : 0) * N;
+    t = t > a.qp_shift ? t - a.qp_shift : 0;
+    rowoff[j] = (t / a.qp_hours) * N;
   }
+  const unsigned char* valid = a.qp_valid;
   // all G loads of a reach are independent and issued together (memory-level parallelism)
 #pragma unroll 2
   for (int i = threadIdx.x; i < nl; i += 1024) {
@@ -869,6 +880,11 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
     R v[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) v[j] = qp[rowoff[j] + ref];
+    if (valid && !valid[ref]) {
+      // a divide missing from the store: the reader's 0.001 fill (readers.py:523-530)
+#pragma unroll
+      for (int j = 0; j < G; ++j) v[j] = R(0.001f);
+    }
     if (fs) {
       const R f = fs[ref];
 #pragma unroll
@@ -909,6 +925,59 @@ __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
   }
   // output[:, 0] = clamp(initial) (mmc.py:412); later steps are sums of clamped states
   out[g * a.T + t] = (t == 0) ? rmax_nan(acc, R(a.qlb)) : acc;
+}
+
+// ============================================================================================
+// Gauge-mode training objective, fused: hourly gauge sums -> trim -> daily area means
+// (scripts/train.py:78-82: downsample(runoff[:, 13 : -11 + tau], num_days), io/functions.py:7-23,
+// F.interpolate(mode="area") = adaptive average pooling: day d averages hours
+// [floor(d L / D), ceil((d + 1) L / D)) of the L-hour trimmed window).  The (G, T) hourly series is
+// never materialised; only (G, D) leaves the kernel.
+// ============================================================================================
+__host__ __device__ inline int64_t pool_start(int64_t d, int64_t L, int64_t D) { return (d * L) / D; }
+__host__ __device__ inline int64_t pool_end(int64_t d, int64_t L, int64_t D) { return ((d + 1) * L + D - 1) / D; }
+
+template <typename R>
+__device__ __forceinline__ R gauge_hour(const GaugeArgs& a, const R* xsave, int64_t g, int64_t t) {
+  R acc = R(0);
+  for (int64_t k = a.goff[g]; k < a.goff[g + 1]; ++k) {
+    const int P = a.pos_of_ref[a.gidx[k]];
+    const BlockDesc B = a.s.blocks[a.block_of_pos[P]];
+    const int r = P - B.pos0;
+    const int64_t tick = t + a.s.off[P];
+    const R x = xsave[a.T * B.pos0 + B.pre_dn + tick * B.nloc + r];
+    acc = acc + ((t == 0 && a.carry) ? x : rmax_nan(x, R(a.qlb)));
+  }
+  return (t == 0) ? rmax_nan(acc, R(a.qlb)) : acc;  // as gauge_reduce_kernel (mmc.py:412, 433-439)
+}
+
+template <typename R>
+__global__ void gauge_daily_kernel(GaugeArgs a, const R* xsave, int64_t t0, int64_t L, int64_t D, R* out) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= a.G * D) return;
+  const int64_t g = w / D, d = w % D;
+  const int64_t h0 = pool_start(d, L, D), h1 = pool_end(d, L, D);
+  R sum = R(0);
+  for (int64_t h = h0; h < h1; ++h) sum = sum + gauge_hour<R>(a, xsave, g, t0 + h);
+  out[w] = sum / R(h1 - h0);  // adaptive_avg_pool: sum / kh / kw with kh = 1
+}
+
+// Adjoint seed of the pooling: dL/dhourly[g, t] = sum over the days d whose window holds t - t0 of
+// dL/ddaily[g, d] / len(d) (ascending d, as adaptive_avg_pool's backward accumulates), 0 outside
+// the trimmed window.  Feeds the gauge-mode routing adjoint.
+template <typename R>
+__global__ void gauge_daily_seed_kernel(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= G * T) return;
+  const int64_t g = w / T, t = w % T, h = t - t0;
+  R acc = R(0);
+  if (h >= 0 && h < L) {
+    const int64_t dc = (h * D) / L;
+    const int64_t dlo = dc > 0 ? dc - 1 : 0, dhi = dc + 1 < D ? dc + 1 : D - 1;
+    for (int64_t d = dlo; d <= dhi; ++d)
+      if (h >= pool_start(d, L, D) && h < pool_end(d, L, D)) acc = acc + gd[g * D + d] / R(pool_end(d, L, D) - pool_start(d, L, D));
+  }
+  gh[w] = acc;
 }
 
 // ============================================================================================
@@ -996,6 +1065,26 @@ hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t 
   return hipGetLastError();
 }
 
+template <typename R>
+hipError_t launch_gauge_daily(const GaugeArgs& a, const R* xsave, int64_t t0, int64_t L, int64_t D, R* out,
+                              hipStream_t stream) {
+  const int64_t total = a.G * D;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(gauge_daily_kernel<R>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a, xsave, t0,
+                     L, D, out);
+  return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_gauge_daily_seed(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh,
+                                   hipStream_t stream) {
+  const int64_t total = G * T;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(gauge_daily_seed_kernel<R>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, G, T, t0,
+                     L, D, gd, gh);
+  return hipGetLastError();
+}
+
 template hipError_t launch_route<float>(const Graph*, const RouteArgs&, bool, hipStream_t);
 template hipError_t launch_route<double>(const Graph*, const RouteArgs&, bool, hipStream_t);
 template int max_resident_blocks<float>(const Graph*, bool);
@@ -1004,5 +1093,13 @@ template hipError_t launch_gather_qprime<float>(const Graph*, RouteArgs&, hipStr
 template hipError_t launch_gather_qprime<double>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_gauge<float>(const GaugeArgs&, const float*, float*, hipStream_t);
 template hipError_t launch_gauge<double>(const GaugeArgs&, const double*, double*, hipStream_t);
+
+template hipError_t launch_gauge_daily<float>(const GaugeArgs&, const float*, int64_t, int64_t, int64_t, float*, hipStream_t);
+template hipError_t launch_gauge_daily<double>(const GaugeArgs&, const double*, int64_t, int64_t, int64_t, double*,
+                                               hipStream_t);
+template hipError_t launch_gauge_daily_seed<float>(int64_t, int64_t, int64_t, int64_t, int64_t, const float*, float*,
+                                                   hipStream_t);
+template hipError_t launch_gauge_daily_seed<double>(int64_t, int64_t, int64_t, int64_t, int64_t, const double*, double*,
+                                                    hipStream_t);
 
 }  // namespace ddr

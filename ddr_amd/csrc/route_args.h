@@ -13,6 +13,9 @@ struct RouteArgs {
   int32_t slot_stride;  // LDS slots per buffer (max nloc + nvirt over blocks)
   int32_t nblocks;      // logical blocks (tickets) of a routing launch
   int32_t p_stride;
+  int32_t qp_hours;               // hourly steps per stored q' row (1, or 24 for a daily store)
+  int32_t qp_shift;               // step t reads q' row max(t - qp_shift, 0): 1 routing, 0 accumulation
+  const unsigned char* qp_valid;  // optional per-reach mask: 0 -> q' = 0.001 (missing divide)
   const void* n;
   const void* q;
   const void* p;
@@ -64,5 +67,15 @@ template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream);
 template <typename R>
 hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t stream);
+template <typename R>
+hipError_t launch_gauge_daily(const GaugeArgs& a, const R* xsave, int64_t t0, int64_t L, int64_t D, R* out,
+                              hipStream_t stream);
+template <typename R>
+hipError_t launch_gauge_daily_seed(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh,
+                                   hipStream_t stream);
+// geometry.hip
+hipError_t launch_geometry_stats(const float* qd, int64_t rs, int64_t ds, int64_t N, int64_t D, const float* n,
+                                 const float* p, int64_t p_stride, const float* q, const float* S, float depth_lb,
+                                 float bw_lb, float* out, hipStream_t stream);
 
 }  // namespace ddr

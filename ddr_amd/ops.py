@@ -62,9 +62,10 @@ def _consts(c: list[float]) -> _lib.Consts:
     return _lib.Consts(*[float(v) for v in c])
 
 
-def _reaches(n, q, p, length, slope, x_storage, flow_scale) -> _lib.Reaches:
+def _reaches(n, q, p, length, slope, x_storage, flow_scale, qp_hours: int = 1, qp_valid=None) -> _lib.Reaches:
     return _lib.Reaches(n.data_ptr(), q.data_ptr(), p.data_ptr(), 1 if p.numel() > 1 else 0, length.data_ptr(),
-                        slope.data_ptr(), x_storage.data_ptr(), flow_scale.data_ptr() if flow_scale is not None else None)
+                        slope.data_ptr(), x_storage.data_ptr(), flow_scale.data_ptr() if flow_scale is not None else None,
+                        int(qp_hours), qp_valid.data_ptr() if qp_valid is not None else None)
 
 
 def _gauges(G, g_off, g_idx, r_off, r_g) -> _lib.Gauges | None:
@@ -108,25 +109,38 @@ def check_status(wait: bool = True) -> None:
 def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Tensor, length: torch.Tensor,
              slope: torch.Tensor, x_storage: torch.Tensor, flow_scale: torch.Tensor | None, q0: torch.Tensor | None,
              g_off: torch.Tensor | None, g_idx: torch.Tensor | None, r_off: torch.Tensor | None,
-             r_g: torch.Tensor | None, graph_id: int, consts: list[float],
-             flags: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+             r_g: torch.Tensor | None, qp_valid: torch.Tensor | None, graph_id: int, consts: list[float], flags: int,
+             steps: int, qp_hours: int, daily: list[int]
+             ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """Returns (runoff, q_last, top_width_last, side_slope_last, x_save, bnd).
 
-    ``r_off``/``r_g`` (reach -> gauge map) are only consumed by the backward."""
+    ``steps`` = T routing steps; ``qprime`` is (T, N), or (ceil(T / 24), N) daily rows with
+    ``qp_hours`` = 24.  Gauge mode (``g_off``/``g_idx``): runoff is (G, T), or with ``daily`` =
+    [t0, L, D] the fused daily objective series (G, D).  ``r_off``/``r_g`` (reach -> gauge map) are
+    only consumed by the backward."""
     _check_inputs(qprime, (("n", n), ("q_spatial", q), ("length", length), ("slope", slope),
                            ("x_storage", x_storage), ("flow_scale", flow_scale), ("q0", q0)), p)
     if p.dtype != qprime.dtype or p.device != qprime.device or not p.is_contiguous():
         raise ValueError("all routing inputs must share dtype/device and be contiguous")
     g = _graph(graph_id)
-    T, N = qprime.shape
+    T, N = int(steps), qprime.shape[1]
+    rows = -(-T // max(1, qp_hours))
+    if qprime.shape[0] < rows:
+        # a daily store may hold more rows than the window routes (the reader keeps the first
+        # (rho - 1) * 24 hours of rho days, readers.py:513-519)
+        raise ValueError(f"streamflow has {qprime.shape[0]} rows, {T} steps at {qp_hours} h per row need {rows}")
     if N != g.n:
         raise ValueError(f"streamflow has {N} reaches, network has {g.n}")
+    if qp_valid is not None and (qp_valid.dtype != torch.uint8 or qp_valid.numel() != N):
+        raise ValueError("qprime_valid must be a uint8 mask of N reaches")
     dev, dt = qprime.device, qprime.dtype
     gauge = g_off is not None
+    if daily and not gauge:
+        raise ValueError("the fused daily objective needs gauge mode (outflow_idx)")
     G = g_off.numel() - 1 if gauge else N
     save = bool(flags & _lib.DDR_FWD_SAVE_X) or gauge
     fflags = flags | (_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_NO_RUNOFF if gauge else 0)
-    runoff = torch.empty((G, T), device=dev, dtype=dt)
+    runoff = torch.empty((G, daily[2] if daily else T), device=dev, dtype=dt)
     x_save = torch.empty(g.save_numel(T), device=dev, dtype=dt)  # always written (runoff is staged here)
     bnd = torch.empty(g.bnd_numel(T), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
@@ -134,30 +148,37 @@ def mc_route(qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Te
     tw = torch.zeros(N, device=dev, dtype=dt)
     ss = torch.zeros(N, device=dev, dtype=dt)
     lib = _lib.load()
-    fwd = lib.ddr_mc_forward_f32 if dt == torch.float32 else lib.ddr_mc_forward_f64
+    f32 = dt == torch.float32
+    fwd = lib.ddr_mc_forward_f32 if f32 else lib.ddr_mc_forward_f64
     stream = _lib.stream_ptr(dev)
-    r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
+    r = _reaches(n, q, p, length, slope, x_storage, flow_scale, qp_hours, qp_valid)
     c = _consts(consts)
     _lib.check(fwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, _lib.ptr(q0), runoff.data_ptr(),
                    x_save.data_ptr(), bnd.data_ptr() if bnd.numel() else None, status.data_ptr(),
                    q_last.data_ptr(), tw.data_ptr(), ss.data_ptr(), int(fflags), stream))
     if gauge:
-        red = lib.ddr_gauge_reduce_f32 if dt == torch.float32 else lib.ddr_gauge_reduce_f64
         gz = _gauges(G, g_off, g_idx, None, None)
-        _lib.check(red(g.handle, x_save.data_ptr(), T, C.byref(gz), float(consts[1]), int(fflags), runoff.data_ptr(),
-                       stream))
+        if daily:
+            red = lib.ddr_gauge_daily_f32 if f32 else lib.ddr_gauge_daily_f64
+            _lib.check(red(g.handle, x_save.data_ptr(), T, C.byref(gz), float(consts[1]), int(fflags), int(daily[0]),
+                           int(daily[1]), int(daily[2]), runoff.data_ptr(), stream))
+        else:
+            red = lib.ddr_gauge_reduce_f32 if f32 else lib.ddr_gauge_reduce_f64
+            _lib.check(red(g.handle, x_save.data_ptr(), T, C.byref(gz), float(consts[1]), int(fflags),
+                           runoff.data_ptr(), stream))
     if _CHECK_STATUS:
         _lib.check(lib.ddr_status_check(1))
     return runoff, q_last, tw, ss, x_save, bnd
 
 
 @mc_route.register_fake
-def _(qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, graph_id, consts, flags):
-    T, N = qprime.shape
+def _(qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, qp_valid, graph_id, consts,
+      flags, steps, qp_hours, daily):
+    T, N = int(steps), qprime.shape[1]
     G = g_off.shape[0] - 1 if g_off is not None else N
     g = _graph(graph_id)
-    return (qprime.new_empty((G, T)), qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N),
-            qprime.new_empty(g.save_numel(T)), qprime.new_empty(g.bnd_numel(T), dtype=torch.float64))
+    return (qprime.new_empty((G, daily[2] if daily else T)), qprime.new_empty(N), qprime.new_empty(N),
+            qprime.new_empty(N), qprime.new_empty(g.save_numel(T)), qprime.new_empty(g.bnd_numel(T), dtype=torch.float64))
 
 
 @torch.library.custom_op("ddrx::mc_route_backward", mutates_args=())
@@ -165,22 +186,33 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
                       p: torch.Tensor, length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor,
                       flow_scale: torch.Tensor | None, x_save: torch.Tensor, bnd: torch.Tensor,
                       r_off: torch.Tensor | None, r_g: torch.Tensor | None, graph_id: int, consts: list[float],
-                      flags: int) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial)."""
+                      flags: int, steps: int, daily: list[int]) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial).  With ``daily`` the incoming gradient
+    is dL/d(daily series) (G, D): its pooling adjoint seeds the gauge-mode routing adjoint."""
     g = _graph(graph_id)
-    T, N = qprime.shape
+    T, N = int(steps), qprime.shape[1]
     dev, dt = qprime.device, qprime.dtype
+    f32 = dt == torch.float32
+    lib = _lib.load()
+    stream = _lib.stream_ptr(dev)
     grad_runoff = grad_runoff.to(dtype=dt).contiguous()
+    if daily:
+        G = grad_runoff.shape[0]
+        if grad_runoff.shape[1] != daily[2]:
+            raise ValueError("daily-series gradient must be (G, D)")
+        hourly = torch.empty((G, T), device=dev, dtype=dt)
+        seed = lib.ddr_gauge_daily_seed_f32 if f32 else lib.ddr_gauge_daily_seed_f64
+        _lib.check(seed(G, T, int(daily[0]), int(daily[1]), int(daily[2]), grad_runoff.data_ptr(), hourly.data_ptr(),
+                        stream))
+        grad_runoff = hourly
+    if grad_runoff.shape[1] != T:
+        raise ValueError("runoff gradient must be (N or G, T)")
     gn = torch.empty(N, device=dev, dtype=dt)
     gq = torch.empty(N, device=dev, dtype=dt)
     gp = torch.empty(N, device=dev, dtype=dt)
-    if grad_runoff.shape[1] != T:
-        raise ValueError("runoff gradient must be (N or G, T)")
     bwd_bnd = torch.empty(g.bwd_numel(T), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
-    lib = _lib.load()
-    bwd = lib.ddr_mc_backward_f32 if dt == torch.float32 else lib.ddr_mc_backward_f64
-    stream = _lib.stream_ptr(dev)
+    bwd = lib.ddr_mc_backward_f32 if f32 else lib.ddr_mc_backward_f64
     r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
     c = _consts(consts)
     gz = None
@@ -197,14 +229,14 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
 
 @mc_route_backward.register_fake
 def _(grad_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g, graph_id, consts,
-      flags):
+      flags, steps, daily):
     N = qprime.shape[1]
     return qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N)
 
 
 def _setup_context(ctx, inputs, output):
-    (qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, graph_id, consts,
-     flags) = inputs
+    (qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r_off, r_g, qp_valid, graph_id, consts,
+     flags, steps, qp_hours, daily) = inputs
     runoff, q_last, tw, ss, x_save, bnd = output
     ctx.graph_id = graph_id
     # strong reference: the registry is weak, and the saved x_save / bnd layouts belong to this
@@ -212,6 +244,8 @@ def _setup_context(ctx, inputs, output):
     ctx.graph = _graph(graph_id)
     ctx.consts = consts
     ctx.flags = flags
+    ctx.steps = steps
+    ctx.daily = list(daily)
     ctx.gauge = g_off is not None
     ctx.p_scalar = p.numel() == 1
     ctx.p_shape = p.shape
@@ -224,11 +258,11 @@ def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
     if g_tw is not None or g_ss is not None:
         if (g_tw is not None and bool(g_tw.ne(0).any())) or (g_ss is not None and bool(g_ss.ne(0).any())):
             raise NotImplementedError("gradients through top_width/side_slope are not supported by ddrx::mc_route")
-    T = qprime.shape[0]
+    T = ctx.steps
     if g_runoff is None:
-        g_runoff = torch.zeros((1 if ctx.gauge else qprime.shape[1], T), device=qprime.device, dtype=qprime.dtype)
         if ctx.gauge:
             raise NotImplementedError("gauge-mode backward needs a runoff gradient")
+        g_runoff = torch.zeros((qprime.shape[1], T), device=qprime.device, dtype=qprime.dtype)
     if g_qlast is not None:
         if ctx.gauge:
             if bool(g_qlast.ne(0).any()):
@@ -238,10 +272,10 @@ def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
             g_runoff = g_runoff.clone()
             g_runoff[:, T - 1] += g_qlast
     gn, gq, gp = mc_route_backward(g_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd,
-                                   r_off, r_g, ctx.graph_id, ctx.consts, ctx.flags)
+                                   r_off, r_g, ctx.graph_id, ctx.consts, ctx.flags, T, ctx.daily)
     if ctx.p_scalar:
         gp = gp.sum().reshape(ctx.p_shape)
-    return None, gn, gq, gp, None, None, None, None, None, None, None, None, None, None, None, None
+    return (None, gn, gq, gp) + (None,) * 16
 
 
 mc_route.register_autograd(_backward, setup_context=_setup_context)
@@ -283,11 +317,37 @@ class GaugeMap:
         return cls(len(idx), t(offs), t(flat), t(roff), t(rg))
 
 
+@dataclass(frozen=True)
+class DailyWindow:
+    """The gauge-mode training objective's window (scripts/train.py:78-82): hours [t0, t0 + L) of the
+    hourly series, area-pooled to D days."""
+
+    t0: int
+    L: int
+    D: int
+
+    @classmethod
+    def for_training(cls, T: int, tau: int = 3) -> "DailyWindow":
+        """runoff[:, 13 : -11 + tau] pooled to len // 24 days (train.py:78-82; tau default 3,
+        configs.py:116-119)."""
+        end = T + (-11 + tau) if (-11 + tau) < 0 else min(T, -11 + tau)
+        L = end - 13
+        if L < 24:
+            raise ValueError(f"T = {T} hours leaves no whole day after the [13 : -11 + tau] trim")
+        return cls(13, L, L // 24)
+
+
 def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor, p: torch.Tensor,
           length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor, *, flow_scale: torch.Tensor | None = None,
           q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
-          save: bool | None = None):
-    """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last)."""
+          save: bool | None = None, steps: int | None = None, qprime_hours: int = 1,
+          qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False):
+    """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last).
+
+    ``qprime_hours`` = 24 with ``steps`` = T routes a daily store (ceil(T / 24), N) indexed in-kernel
+    (readers.py:513-519); ``qprime_valid`` (N, bool) marks divides present in the store, the others get
+    0.001 (readers.py:523-530).  ``daily`` (gauge mode) returns the fused daily objective series
+    (G, D).  ``accumulate`` makes every step a hot start (geometry_predictor.py:193-212)."""
     dt = qprime.dtype
     dev = qprime.device
 
@@ -296,13 +356,18 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
 
     n, q, p, length, slope, x_storage, flow_scale, q0 = map(prep, (n, q, p, length, slope, x_storage, flow_scale, q0))
     p = p.reshape(-1) if p.numel() > 1 else p.reshape(1)
+    if steps is None:
+        steps = qprime.shape[0] * max(1, qprime_hours)
     if save is None:
-        save = torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
-    flags = (_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
+        save = (not accumulate) and torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
+    flags = ((_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
+             | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0))
+    valid = None if qprime_valid is None else qprime_valid.to(device=dev, dtype=torch.uint8).contiguous()
     gid = register_graph(graph)
     gz = gauges
     out = mc_route(qprime.contiguous(), n, q, p, length, slope, x_storage, flow_scale, q0,
                    gz.offsets if gz else None, gz.index if gz else None, gz.reach_offsets if gz else None,
-                   gz.reach_gauges if gz else None, gid, consts.as_list(), flags)
+                   gz.reach_gauges if gz else None, valid, gid, consts.as_list(), flags, int(steps), int(qprime_hours),
+                   [daily.t0, daily.L, daily.D] if daily is not None else [])
     runoff, q_last, tw, ss, _, _ = out
     return runoff, q_last, tw, ss

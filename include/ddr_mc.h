@@ -121,6 +121,11 @@ typedef struct {
   const void* slope;       /* already clamped at the slope minimum     (N)   */
   const void* x_storage;   /* Muskingum X                               (N)   */
   const void* flow_scale;  /* optional per-reach q' multiplier (N) or NULL    */
+  int64_t qprime_hours;    /* hours per stored q' row: 0/1 hourly (T, N); 24 a daily */
+                           /* store (ceil(T / 24), N), indexed q'[t / 24] in-kernel, */
+                           /* the reader's repeat(24) (readers.py:513-519)           */
+  const uint8_t* qprime_valid; /* optional (N): 0 = divide missing from the store, */
+                           /* its q' is 0.001 (readers.py:523-530); NULL = all valid */
 } ddr_mc_reaches;
 
 /* Gauge mode: out[g, t] = sum_{k in [off[g], off[g+1])} Q_t[idx[k]] (device int64 arrays,
@@ -134,8 +139,11 @@ typedef struct {
   const int64_t* reach_gauges;   /* (offsets[G]) gauge id of each membership      */
 } ddr_gauges;
 
-/* DDR_FWD_SAVE_X is accepted for compatibility: x_save is always written. */
-enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4 };
+/* DDR_FWD_SAVE_X is accepted for compatibility: x_save is always written.
+ * DDR_FWD_ACCUMULATE: every step is a hot start, Q_t = max((I - N)^-1 q'_t, q_lb) with step t
+ * reading q' row t -- the per-day discharge accumulation of scripts/geometry_predictor.py:193-212
+ * (compute_hotstart_discharge, mmc.py:25-66) for all days in one launch. */
+enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8 };
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
  * Returns DDR_ERR_TIMEOUT instead of launching when an earlier launch's hand-off timed out
@@ -182,6 +190,34 @@ ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t
 ddr_status ddr_gauge_reduce_f64(const ddr_graph* g, const double* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,
                                 double* runoff, void* stream);
+
+/* Gauge-mode training objective, fused (scripts/train.py:78-82 + io/functions.py:7-23): daily area
+ * means of the gauge sums over the trimmed window [t0, t0 + L) of the routed states x_save,
+ * out (G, D): day d averages hours t0 + [floor(d L / D), ceil((d + 1) L / D)) like
+ * F.interpolate(mode="area").  The reference trims runoff[:, 13 : -11 + tau] and pools to
+ * D = L // 24 days: t0 = 13, L = T - 24 + tau. */
+ddr_status ddr_gauge_daily_f32(const ddr_graph* g, const float* x_save, int64_t T, const ddr_gauges* gauges,
+                               double discharge_lb, int32_t flags, int64_t t0, int64_t L, int64_t D,
+                               float* daily, void* stream);
+ddr_status ddr_gauge_daily_f64(const ddr_graph* g, const double* x_save, int64_t T, const ddr_gauges* gauges,
+                               double discharge_lb, int32_t flags, int64_t t0, int64_t L, int64_t D,
+                               double* daily, void* stream);
+/* Its adjoint: dL/d(hourly gauge series) (G, T) from dL/d(daily) (G, D), the seed of the gauge-mode
+ * ddr_mc_backward (zero outside the trimmed window). */
+ddr_status ddr_gauge_daily_seed_f32(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D,
+                                    const float* grad_daily, float* grad_hourly, void* stream);
+ddr_status ddr_gauge_daily_seed_f64(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D,
+                                    const double* grad_daily, double* grad_hourly, void* stream);
+
+/* Per-reach temporal statistics of the trapezoid geometry (src/ddr/geometry/statistics.py:20-83):
+ * q_daily holds the daily accumulated discharge, element (reach, day) at
+ * reach * reach_stride + day * day_stride (1 <= days <= 512); out is (24, n): for the variables
+ * depth, top_width, bottom_width, side_slope, hydraulic_radius, discharge (in this order) the rows
+ * min, max, median, mean (NaN skipped as numpy's nan* reductions).  Device pointers, float32. */
+ddr_status ddr_geometry_stats_f32(const float* q_daily, int64_t reach_stride, int64_t day_stride, int64_t n,
+                                  int64_t days, const float* n_manning, const float* p_spatial,
+                                  int64_t p_stride, const float* q_spatial, const float* slope,
+                                  double depth_lb, double bottom_width_lb, float* out, void* stream);
 
 /* Synchronise `stream` and read the device status block written by the last launches:
  * returns DDR_OK or DDR_ERR_TIMEOUT. */

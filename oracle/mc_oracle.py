@@ -379,6 +379,82 @@ def gauge_reduce(Qall: np.ndarray, outflow_idx) -> np.ndarray:
     return out
 
 
+def area_downsample(x: np.ndarray, days: int) -> np.ndarray:
+    """``functions.py:7-23`` ``F.interpolate(x.unsqueeze(1), size=(days,), mode="area")`` restated:
+    adaptive average pooling, day d averages [floor(d L / D), ceil((d + 1) L / D)) -- summed in order,
+    then divided by the window length (x: (G, L))."""
+    G, L = x.shape
+    out = np.zeros((G, days), dtype=x.dtype)
+    for d in range(days):
+        a, b = (d * L) // days, ((d + 1) * L + days - 1) // days
+        acc = np.zeros(G, dtype=x.dtype)
+        for h in range(a, b):
+            acc = acc + x[:, h]
+        out[:, d] = acc / x.dtype.type(b - a)
+    return out
+
+
+def daily_l1_objective(gauge_runoff: np.ndarray, obs: np.ndarray, tau: int = 3, warmup: int = 3):
+    """``scripts/train.py:78-97``: trim [13 : -11 + tau], pool to len // 24 days, drop gauges whose
+    observations have a NaN, L1 against obs (already cut to the routed days), skipping ``warmup``
+    days.  Returns (loss, daily (G, D), dloss/d(gauge_runoff) (G, T)) -- the last by the chain rule of
+    the mean absolute error through the pooling, fp64."""
+    G, T = gauge_runoff.shape
+    trimmed = gauge_runoff[:, 13:(-11 + tau) if (-11 + tau) < 0 else (-11 + tau)]
+    L = trimmed.shape[1]
+    D = L // 24
+    daily = area_downsample(trimmed, D)
+    keep = ~np.isnan(obs).any(axis=1)
+    pred = daily[keep][:, warmup:].astype(np.float64)
+    target = obs[keep][:, warmup:].astype(np.float64)
+    diff = pred - target
+    loss = float(np.abs(diff).mean())
+    gd = np.zeros((G, D), dtype=np.float64)
+    gd[np.flatnonzero(keep)[:, None], np.arange(warmup, D)[None, :]] = np.sign(diff) / diff.size
+    gh = np.zeros((G, T), dtype=np.float64)
+    for d in range(D):
+        a, b = (d * L) // D, ((d + 1) * L + D - 1) // D
+        gh[:, 13 + a:13 + b] += gd[:, d:d + 1] / (b - a)
+    return loss, daily, gh
+
+
+def accumulate_daily(net: Network, q_daily: np.ndarray, bd: Bounds = Bounds()) -> np.ndarray:
+    """``scripts/geometry_predictor.py:193-212``: per day d, Q_d = compute_hotstart_discharge(
+    max(q'_d, q_lb)) = max((I - N)^{-1} max(q'_d, q_lb), q_lb) -- (n_days, N) float32."""
+    f = np.float32
+    out = np.zeros(q_daily.shape, dtype=f)
+    for d in range(q_daily.shape[0]):
+        out[d] = hotstart(net, np.maximum(np.asarray(q_daily[d], f), f(bd.discharge)), bd, f)
+    return out
+
+
+def geometry_statistics(n, p, q, slope, daily_q: np.ndarray, bd: Bounds = Bounds()) -> dict:
+    """``src/ddr/geometry/statistics.py:20-83``: per-day trapezoid geometry (trapezoidal.py:62-97, fp32
+    reference order, correctly rounded pow) and per-reach nanmin / nanmax / nanmedian / nanmean over
+    the days, for depth, top_width, bottom_width, side_slope, hydraulic_radius and discharge."""
+    f = np.float32
+    D, N = daily_q.shape
+    geo = {k: np.empty((D, N), dtype=f) for k in ("depth", "top_width", "bottom_width", "side_slope",
+                                                    "hydraulic_radius")}
+    for d in range(D):
+        g = trapezoid_celerity(np.asarray(daily_q[d], f), np.asarray(n, f), np.asarray(q, f), np.asarray(p, f),
+                               np.asarray(slope, f), bd, f, full=True)
+        geo["depth"][d], geo["top_width"][d], geo["bottom_width"][d] = g["depth"], g["tw"], g["bw"]
+        geo["side_slope"][d], geo["hydraulic_radius"][d] = g["ss"], g["R"]
+    out = {}
+    with np.errstate(all="ignore"):
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            for name, arr in [*geo.items(), ("discharge", np.asarray(daily_q, f))]:
+                out[f"{name}_min"] = np.nanmin(arr, axis=0).astype(f)
+                out[f"{name}_max"] = np.nanmax(arr, axis=0).astype(f)
+                out[f"{name}_median"] = np.nanmedian(arr, axis=0).astype(f)
+                out[f"{name}_mean"] = np.nanmean(arr, axis=0).astype(f)
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # Adjoint (hand derived, SURVEY Appendix A) -- fp64
 # ---------------------------------------------------------------------------------------------

@@ -14,8 +14,13 @@ Fixtures:
   gauge.npz     F4  gauge mode (ragged outflow_idx incl. a negative index) + carry_state batch 2
   c1.npz        F5  config C1 shape (2000 x 720): outlet series, sampled runoff, unit-param grads
   csr.npz       F6  canonical CSR + PatternMapper (crow, col) for the F3 and F5 graphs
+  geostats.npz  F7  reference compute_geometry_statistics (statistics.py:20-83): 150 reaches x 31 and
+                    x 30 days (odd / even median), NaN discharge entries, default and mock bounds
+  daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
+                    downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
+                    warmup 3, and torch autograd's d loss / d runoff
 
-Run:  python tests/golden/make_golden.py
+Run:  python tests/golden/make_golden.py [geostats daily]   (no argument: all fixtures)
 """
 
 from __future__ import annotations
@@ -163,7 +168,73 @@ def case(mmc, params, net, T, seed, outflow_idx=None, learn_p=True):
     return inputs, res, mc, dc
 
 
+def load_objective_modules():
+    """statistics.py (needs ddr.geometry.trapezoidal) and io/functions.py, with stub parents."""
+    load_reference()
+    spec = importlib.util.spec_from_file_location("ddr.geometry.statistics", REF / "geometry/statistics.py")
+    stats = importlib.util.module_from_spec(spec)
+    sys.modules["ddr.geometry.statistics"] = stats
+    spec.loader.exec_module(stats)
+    spec = importlib.util.spec_from_file_location("ddr_io_functions", REF / "io/functions.py")
+    fun = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fun)
+    return stats, fun
+
+
+def make_geostats():
+    stats, _ = load_objective_modules()
+    rng = np.random.default_rng(77)
+    N = 150
+    u = synthetic.unit_parameters(N, 77)
+    n = (u["n"] * np.float32(0.235) + np.float32(0.015)).astype(np.float32)
+    q = u["q_spatial"].astype(np.float32)
+    lo, hi = np.log(np.float32(1.0 + 1e-6)), np.log(np.float32(200.0))
+    p = np.exp(u["p_spatial"] * np.float32(hi - lo) + np.float32(lo)).astype(np.float32)
+    slope = np.maximum(rng.lognormal(np.log(1e-3), 1.0, N).astype(np.float32), np.float32(1e-3))
+    out = dict(n=n, p=p, q=q, slope=slope)
+    for D in (31, 30):
+        dq = rng.lognormal(np.log(5.0), 1.5, (D, N)).astype(np.float32)
+        dq[rng.random((D, N)) < 0.02] = np.nan
+        dq[:, 7] = np.nan  # a reach with no valid day
+        for tag, mins in (("default", {"depth": 0.01, "bottom_width": 0.01}), ("mock", {"depth": 0.01, "bottom_width": 0.1})):
+            with np.errstate(all="ignore"):
+                import warnings
+
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore", RuntimeWarning)
+                    res = stats.compute_geometry_statistics(torch.from_numpy(n), torch.from_numpy(p), torch.from_numpy(q),
+                                                            torch.from_numpy(slope), dq, mins)
+            for k, v in res.items():
+                out[f"d{D}_{tag}_{k}"] = v
+        out[f"d{D}_q"] = dq
+    np.savez_compressed(HERE / "geostats.npz", **out)
+
+
+def make_daily():
+    _, fun = load_objective_modules()
+    rng = np.random.default_rng(88)
+    G, T, tau, warmup = 7, 2136, 3, 3
+    runoff = torch.from_numpy(rng.lognormal(np.log(10.0), 1.0, (G, T)).astype(np.float32)).requires_grad_(True)
+    num_days = len(runoff[0][13:(-11 + tau)]) // 24
+    daily = fun.downsample(runoff[:, 13:(-11 + tau)], rho=num_days)
+    obs = rng.lognormal(np.log(10.0), 1.0, (G, num_days)).astype(np.float32)
+    obs[2, 40] = np.nan  # gauge 2 is dropped (train.py:84-90)
+    keep = ~np.isnan(obs).any(axis=1)
+    pred = daily[torch.from_numpy(keep)]
+    target = torch.from_numpy(obs[keep])
+    loss = torch.nn.functional.l1_loss(input=pred.transpose(0, 1)[warmup:].unsqueeze(2),
+                                       target=target.transpose(0, 1)[warmup:].unsqueeze(2))
+    loss.backward()
+    np.savez_compressed(HERE / "daily.npz", runoff=runoff.detach().numpy(), obs=obs, tau=np.int64(tau),
+                        warmup=np.int64(warmup), ref_daily=daily.detach().numpy(), ref_loss=np.float32(loss.item()),
+                        ref_grad=runoff.grad.numpy())
+
+
 def main():
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            {"geostats": make_geostats, "daily": make_daily}[name]()
+        return
     torch.manual_seed(0)
     utils, mmc = load_reference()
     np.savez_compressed(HERE / "kat.npz", **kat(utils, mmc))
@@ -212,6 +283,8 @@ def main():
     np.savez_compressed(HERE / "csr.npz", t300_crow=c3[0], t300_col=c3[1], t300_mcrow=c3[2], t300_mcol=c3[3],
                         t300_mapidx=c3[4], c1_crow=c5[0], c1_col=c5[1], c1_mcrow=c5[2], c1_mcol=c5[3],
                         c1_mapidx=c5[4])
+    make_geostats()
+    make_daily()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

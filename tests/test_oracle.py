@@ -110,3 +110,26 @@ def test_scipy_recipe_equals_level_sweep():
     r = case.reaches()
     ra, rb = O.route(a, r, case.qprime), O.route(b, r, case.qprime)
     np.testing.assert_array_equal(ra["runoff"], rb["runoff"])
+
+
+def test_geometry_statistics_oracle_matches_reference_golden():
+    """oracle.geometry_statistics restates statistics.py:20-83 (fixture from the reference itself)."""
+    d = load_golden("geostats")
+    for D in (31, 30):
+        for tag, bd in (("default", O.Bounds()), ("mock", O.Bounds(bottom_width=0.1))):
+            got = O.geometry_statistics(d["n"], d["p"], d["q"], d["slope"], d[f"d{D}_q"], bd)
+            for k, v in got.items():
+                ref = d[f"d{D}_{tag}_{k}"]
+                assert np.array_equal(np.isnan(v), np.isnan(ref)), k
+                ok = ~np.isnan(ref)
+                # correctly rounded pow vs the reference's 1-ulp Sleef powf
+                assert maxrel(v[ok], ref[ok]) <= 2e-6, (D, tag, k)
+
+
+def test_daily_objective_oracle_matches_reference_golden():
+    """oracle.daily_l1_objective restates train.py:78-97 (downsample + NaN-gauge mask + L1 + warmup)."""
+    d = load_golden("daily")
+    loss, daily, grad = O.daily_l1_objective(d["runoff"], d["obs"], int(d["tau"]), int(d["warmup"]))
+    assert maxrel(daily, d["ref_daily"]) <= 1e-6
+    assert abs(loss - float(d["ref_loss"])) <= 1e-6 * abs(float(d["ref_loss"]))
+    assert maxrel(grad, d["ref_grad"], floor=1e-12) <= 1e-6
