@@ -1,17 +1,27 @@
-"""Headline benchmark: differentiable Muskingum-Cunge routing, forward + backward.
+"""Headline benchmark: differentiable Muskingum-Cunge routing on MI355X (BASELINE.json configs).
 
-Metric (BASELINE.json): reach-timesteps/s fwd+bwd on a CONUS-shaped network (Hydrofabric-like,
-800k reaches, ~3k outlet basins, largest basin 0.35 N, deep Hack's-law main stems) over an 8760-hour
-water year (config C5), plus the fraction of HBM peak of the dominant kernel.
+Workloads (``--workload``; the default is the headline metric):
 
-One "step" = one full forward (hot start + 8759 routing steps) and one full backward (adjoint w.r.t.
-n, q_spatial, p_spatial) over the whole water year, with loss = sum(W * runoff), W ~ U(0, 1).
+* ``c5`` -- BASELINE metric: forward + backward over an 8760-hour water year of a Hydrofabric-shaped
+  CONUS network (800k reaches, 3000 outlet basins, Zipf sizes with the largest 0.35 N, Hack's-law main
+  stems, 35 % single-inflow reaches), loss = sum(W * runoff).  One step = one full forward (hot start +
+  8759 routing steps) and one full adjoint (gradients w.r.t. n, q_spatial, p_spatial).
+* ``c3`` -- the training batch: 256 gauged subnetworks (log-uniform 100..20k reaches), rho = 90 days
+  (T = 2136 h), one gauge per subnetwork outlet.  One step = parameter network forward (a KAN
+  stand-in: pykan is not installed here) -> denormalize -> fused gauge-mode routing with the daily
+  objective (trim [13 : -11 + tau], area pooling) -> L1 loss vs synthetic observations -> backward ->
+  RCCL all-reduce of the network's gradients -> clip + Adam step (scripts/train.py:54-104).
+* ``c4`` -- MERIT-CONUS-shaped network (350k reaches, ~1k outlets, x = 0.3): water-year forward route
+  + per-day accumulation and geometry statistics over the 365 days (geometry_predictor.py:176-212).
+* ``c2`` -- one 5k-reach gauged subnetwork, water-year forward route, parameters fixed.
 
-Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): weak scaling -- the global forest has
-N x (C5-shaped forest); outlet basins are LPT-sharded across ranks (no data-path collective; basins
-are independent).  Barrier + synchronize bracket the K timed steps; time is the max over ranks.
+Multi-GPU (``torchrun --nproc-per-node N bench.py --gpus N``): STRONG scaling -- every rank builds the
+same global network and routes the outlet basins LPT-assigned to it (no data-path collective: basins
+are independent).  RCCL carries the C3 gradient all-reduce and the timing/size
+reductions.  Barrier + synchronize bracket the K timed steps; the time is the max over ranks; value =
+all ranks' reach-steps / that time.
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--reaches 800000] [--T 8760]
+Usage:  python bench.py [--workload c5] [--gpus N] [--steps K] [--warmup W]
 """
 
 from __future__ import annotations
@@ -31,69 +41,374 @@ import torch
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-from ddr_amd import synthetic  # noqa: E402
+from ddr_amd import _lib, synthetic  # noqa: E402
 from ddr_amd.graph import RiverGraph  # noqa: E402
-from ddr_amd.ops import RouteConsts, route  # noqa: E402
-from ddr_amd.partition import shard_basins  # noqa: E402
+from ddr_amd.ops import DailyWindow, GaugeMap, RouteConsts, route  # noqa: E402
+from ddr_amd.partition import extract_basins, shard_basins  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
-FWD_BYTES = 12  # q' read + runoff write + x_save write per reach-step
-BWD_BYTES = 12  # grad read + x_save read + q' read per reach-step
 RANGES = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
+
+WORKLOADS = {
+    "c5": dict(metric="reach-timesteps/sec fwd+bwd (CONUS 800k reaches, 8760 h)", T=8760, grad=True,
+               desc="C5: Hydrofabric-shaped CONUS network, fwd+bwd over a water year"),
+    "c3": dict(metric="reach-timesteps/sec fwd+bwd (256 gauged subnetworks, KAN backprop, RCCL grad all-reduce)",
+               T=2136, grad=True, desc="C3: training batch of 256 gauged subnetworks (rho 90 d), daily L1 objective"),
+    "c4": dict(metric="reach-timesteps/sec fwd (MERIT-CONUS 350k reaches, 8760 h) + 365-day geometry statistics",
+               T=8760, grad=False, desc="C4: MERIT-shaped network, water-year forward + geometry statistics"),
+    "c2": dict(metric="reach-timesteps/sec fwd (5k-reach gauged subnetwork, 8760 h, parameters fixed)", T=8760,
+               grad=False, desc="C2: one Hack-law subnetwork, water-year forward"),
+}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_rank_network(args, rank: int, world: int):
-    """This rank's basins of a world x C5 forest (Zipf sizes, largest 0.35 of each C5 block)."""
-    sizes = np.concatenate([synthetic.zipf_sizes(args.reaches, args.basins, args.largest) for _ in range(world)])
-    owner = shard_basins(sizes, world)
-    mine = np.sort(owner[rank])
-    my_sizes = sizes[mine]
-    net = synthetic.forest(my_sizes, seed=args.seed + 7919 * rank, single_inflow=args.single_inflow)
-    return net, int(sizes.sum())
+def global_network(args):
+    """The workload's whole network (deterministic: every rank builds the same one)."""
+    w = args.workload
+    if w == "c5":
+        sizes = synthetic.zipf_sizes(args.reaches, args.basins, args.largest)
+        return synthetic.forest(sizes, seed=5, single_inflow=0.35), None
+    if w == "c3":
+        return synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 3), seed=3, single_inflow=0.25), None
+    if w == "c4":
+        return synthetic.forest(synthetic.zipf_sizes(350_000, 1000, 0.35), seed=4, single_inflow=0.15), 0.3
+    return synthetic.hack_basin(5000, seed=2), None
 
 
-def cpu_baseline(args):
-    """Time the oracle port of the reference recipe on a bounded sample (1 core)."""
+def shard(net, rank, world):
+    """Reaches (global ids, ascending) and sub-network of the basins LPT-assigned to this rank."""
+    starts = np.concatenate([[0], np.cumsum(net.basin_sizes)[:-1]])
+    mine = np.sort(shard_basins(net.basin_sizes, world)[rank])
+    keep = np.zeros(net.n, bool)
+    for b in mine:
+        keep[starts[b]:starts[b] + net.basin_sizes[b]] = True
+    n_sub, rows, cols, ids = extract_basins(net.n, net.rows, net.cols, keep)
+    return n_sub, rows, cols, ids, mine
+
+
+class ParamNet(torch.nn.Module):
+    """KAN stand-in for C3 (pykan is not installed): attributes -> (n, q_spatial, p_spatial) in [0, 1]
+    through sigmoid, the reference nn's output contract (src/ddr/nn/kan.py:11-62); ~35k parameters."""
+
+    def __init__(self, n_attr=10, hidden=128):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)  # identical replicas on every rank
+        self.layers = torch.nn.ModuleList([torch.nn.Linear(n_attr, hidden), torch.nn.Linear(hidden, hidden),
+                                           torch.nn.Linear(hidden, hidden), torch.nn.Linear(hidden, 3)])
+        with torch.no_grad():
+            for m in self.layers:
+                m.weight.copy_(torch.randn(m.weight.shape, generator=g) / math.sqrt(m.weight.shape[1]))
+                m.bias.zero_()
+
+    def forward(self, x):
+        for m in self.layers[:-1]:
+            x = torch.nn.functional.silu(m(x))
+        return torch.sigmoid(self.layers[-1](x))
+
+
+def denorm(un, uq, up):
+    """utils.py:166-185 (torch, autograd reaches the unit-interval parameters)."""
+    n = un * (RANGES["n"][1] - RANGES["n"][0]) + RANGES["n"][0]
+    q = uq * (RANGES["q_spatial"][1] - RANGES["q_spatial"][0]) + RANGES["q_spatial"][0]
+    lo, hi = math.log(RANGES["p_spatial"][0] + 1e-6), math.log(RANGES["p_spatial"][1])
+    return n, q, torch.exp(up * (hi - lo) + lo)
+
+
+def cpu_baseline(args, net_global, x_const):
+    """The oracle port of the reference recipe, one core, on a bounded sample of the workload."""
     from oracle import mc_oracle as O
 
     os.environ.setdefault("OMP_NUM_THREADS", "1")
-    sample_n, sample_T = args.cpu_reaches, args.cpu_T
-    net = synthetic.forest(synthetic.zipf_sizes(sample_n, max(1, args.basins * sample_n // args.reaches),
-                                                args.largest), seed=args.seed, single_inflow=args.single_inflow)
-    no = O.Network.from_coo(net.n, net.rows, net.cols)
+    w = args.workload
+    if w == "c5":
+        sample = synthetic.forest(synthetic.zipf_sizes(args.cpu_reaches, max(1, args.basins * args.cpu_reaches // args.reaches),
+                                                       args.largest), seed=5, single_inflow=0.35)
+    elif w == "c3":
+        sample = synthetic.forest(synthetic.loguniform_sizes(12, 100, 20000, 3), seed=3, single_inflow=0.25)
+    elif w == "c4":
+        sample = synthetic.forest(synthetic.zipf_sizes(20_000, 60, 0.35), seed=4, single_inflow=0.15)
+    else:
+        sample = synthetic.hack_basin(5000, seed=2)
+    T = args.cpu_T
+    no = O.Network.from_coo(sample.n, sample.rows, sample.cols)
     no.solver = "scipy"
-    at = synthetic.reach_attributes(net.n, args.seed)
-    u = synthetic.unit_parameters(net.n, args.seed)
+    at = synthetic.reach_attributes(sample.n, 7, x_const=x_const)
+    u = synthetic.unit_parameters(sample.n, 7)
     r = O.Reaches(O.denormalize(u["n"], RANGES["n"]), O.denormalize(u["q_spatial"], RANGES["q_spatial"]),
                   O.denormalize(u["p_spatial"], RANGES["p_spatial"], True), at.length,
                   np.maximum(at.slope, np.float32(1e-3)), at.x)
-    qp = synthetic.lateral_inflow(net.n, sample_T, args.seed)
-    W = np.random.default_rng(1).uniform(0, 1, (net.n, sample_T)).astype(np.float32)
+    qp = synthetic.lateral_inflow(sample.n, T, 7)
+    grad = WORKLOADS[w]["grad"]
     t0 = time.perf_counter()
     res = O.route(no, r, qp, O.Bounds(), dtype=np.float32)
-    O.route_backward(no, r, qp, res["x"], W, O.Bounds())
+    if grad:
+        W = np.random.default_rng(1).uniform(0, 1, (sample.n, T)).astype(np.float32)
+        O.route_backward(no, r, qp, res["x"], W, O.Bounds())
     el = time.perf_counter() - t0
-    return {"value": net.n * (sample_T - 1) / el, "unit": "reach-timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{net.n} reaches x {sample_T} h C5-shaped sub-forest, fwd (fp32 + SciPy fp64 "
-                      f"spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve), {el:.1f} s"}
+    what = ("fwd (fp32 + SciPy fp64 spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve)"
+            if grad else "fwd (fp32 + SciPy fp64 spsolve_triangular per step)")
+    return {"value": sample.n * (T - 1) / el, "unit": "reach-timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s"}
 
 
-def measured_traffic(kernel: str, args) -> float | None:
-    """HBM bytes per launch of `kernel` from the committed PMC measurement (profiles/), if it was taken
-    on this workload; None otherwise (rocprofv3 counters cannot be read from inside the run)."""
-    f = ROOT / "profiles" / "r01_traffic_c5.json"
+def counter_file(args, lib_hash):
+    """PMC summary of this workload for the loaded library build (profiles/, made by tools/pmc.sh +
+    tools/pmc_to_json.py); None when absent or stale (another build or configuration)."""
+    f = ROOT / "profiles" / "counters" / f"{args.workload}.json"
     try:
         d = json.loads(f.read_text())
     except (OSError, ValueError):
         return None
-    if d.get("config") != {"reaches_per_gpu": args.reaches, "T": args.T} or args.dtype != "f32":
+    if d.get("build") != lib_hash or d.get("T") != args.T or d.get("reaches") != args.reaches_total:
         return None
-    k = d["kernels"].get(kernel)
-    return None if k is None else float(k["bytes_per_launch"])
+    return d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c5", choices=sorted(WORKLOADS))
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reaches", type=int, default=800_000, help="C5 network size")
+    ap.add_argument("--basins", type=int, default=3000)
+    ap.add_argument("--largest", type=float, default=0.35)
+    ap.add_argument("--T", type=int, default=0, help="override the workload's hours")
+    ap.add_argument("--tau", type=int, default=3)
+    ap.add_argument("--warmup-days", type=int, default=3)
+    ap.add_argument("--cpu-reaches", type=int, default=40_000)
+    ap.add_argument("--cpu-T", type=int, default=720)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dropin-steps", type=int, default=2, help="C5, 1 GPU: also time the drop-in dmc() path")
+    ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
+    args = ap.parse_args()
+    spec = WORKLOADS[args.workload]
+    T = args.T or spec["T"]
+    args.T = T
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+
+    t_setup = time.perf_counter()
+    net, x_const = global_network(args)
+    args.reaches_total = net.n
+    n_loc, rows, cols, ids, my_basins = shard(net, rank, world) if world > 1 else (
+        net.n, net.rows, net.cols, np.arange(net.n), np.arange(len(net.basin_sizes)))
+    g = RiverGraph(n_loc, rows, cols, steps_hint=T)
+    log(f"[rank {rank}] {g} ({len(my_basins)} basins) built in {time.perf_counter() - t_setup:.1f}s")
+    at = synthetic.reach_attributes(net.n, 11, x_const=x_const)
+    u = synthetic.unit_parameters(net.n, 11)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a)[ids])).to(dev)  # noqa: E731
+    length, slope, xs = tt(at.length), tt(np.maximum(at.slope, np.float32(1e-3))), tt(at.x)
+    qprime = synthetic.lateral_inflow_torch(net.n, T, seed=11, device=dev, ids=ids)
+    consts = RouteConsts()
+    lib = _lib.load()
+    lib_hash = lib.ddr_version().decode().split()[-1]
+    fwd_bytes, bwd_bytes = (8, 8) if args.workload == "c3" else (12, 12)  # SURVEY §8(d); gauge mode: no runoff
+
+    # ---- the step of each workload --------------------------------------------------------------------
+    if args.workload == "c5":
+        u_n, u_q, u_p = (tt(u[k]).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial"))
+        gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+        W = torch.rand((n_loc, T), device=dev, dtype=torch.float32, generator=gen)  # dL/drunoff of sum(W * runoff)
+
+        def step():
+            for t_ in (u_n, u_q, u_p):
+                t_.grad = None
+            n, q, p = denorm(u_n, u_q, u_p)
+            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts)
+            runoff.backward(W)
+
+    elif args.workload == "c3":
+        from ddr_amd.distributed import allreduce_gradients
+
+        feats = tt(synthetic.reach_features(net.n, seed=11))
+        model = ParamNet().to(dev)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        outlets = np.flatnonzero(np.asarray(synthetic.SyntheticNetwork(n_loc, rows, cols, np.array([n_loc])).down) < 0)
+        gz = GaugeMap.build([np.array([o]) for o in outlets], n_loc, dev)
+        window = DailyWindow.for_training(T, args.tau)
+        G_global = len(net.basin_sizes)
+        obs = torch.from_numpy(np.random.default_rng(100).lognormal(np.log(5.0), 1.0, (G_global, window.D))
+                               .astype(np.float32)[my_basins]).to(dev)
+        wd = args.warmup_days
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            un = model(feats)
+            n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
+            daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts)
+            # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
+            loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
+            loss.backward()
+            allreduce_gradients(list(model.parameters()))  # RCCL, one flat bucket
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            opt.step()
+
+    else:
+        from ddr_amd.geometry.statistics import geometry_statistics_from_inflow
+
+        n, q, p = denorm(tt(u["n"]), tt(u["q_spatial"]), tt(u["p_spatial"]))
+
+        def step():
+            with torch.no_grad():
+                if args.workload == "c4":  # first: the kernel timer reports the last forward launch
+                    geometry_statistics_from_inflow(g, qprime[::24][:365], n, p, q, slope)
+                route(g, qprime, n, q, p, length, slope, xs, consts=consts, save=False)
+
+    ev = []
+    kms = {"forward": [], "backward": []}  # main routing kernels, HIP events on the launch stream
+
+    def timed_step():
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        ev.append((e0, e1))
+        for w_, key in ((0, "forward"), (1, "backward")):
+            if key == "backward" and not spec["grad"]:
+                continue
+            ms = ctypes.c_float()
+            _lib.check(lib.ddr_kernel_ms(w_, ctypes.byref(ms)))
+            kms[key].append(ms.value)
+
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] inputs resident ({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB); warmup {args.warmup}")
+    for _ in range(args.warmup):
+        step()
+    _lib.check(lib.ddr_set_kernel_timing(1))
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        timed_step()
+        log(f"[rank {rank}] step {i + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.check(lib.ddr_set_kernel_timing(0))
+    _lib.check(lib.ddr_status_check(1))  # any timed-out hand-off fails the run
+    if args.block_profile and rank == 0:
+        block_profile(args.block_profile, g, step, lib)
+
+    # ---- reductions over ranks ------------------------------------------------------------------------
+    sizes = torch.zeros(max(world, 1), device=dev, dtype=torch.float64)
+    sizes[rank] = n_loc
+    tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(sizes, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    sizes = sizes.cpu().numpy()
+    elapsed = float(tmax.item())
+    total_reaches = int(sizes.sum())
+    value = total_reaches * (T - 1) * args.steps / elapsed
+
+    if rank == 0:
+        step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        reach_steps = n_loc * (T - 1)
+        kern = {}
+        for key, nb in (("forward", fwd_bytes), ("backward", bwd_bytes)):
+            if kms[key]:
+                k = float(np.mean(kms[key]))
+                kern[key] = {"kernel_ms": k, "GB/s": nb * reach_steps / (k * 1e-3) / 1e9, "bytes_per_reach_step": nb}
+        dom = max(kern, key=lambda k_: kern[k_]["kernel_ms"])
+        achieved = kern[dom]["GB/s"]
+        cf = counter_file(args, lib_hash)
+        kc = (cf or {}).get("kernels", {}).get(f"route_{dom}_kernel", {})
+        dropin = None
+        if args.workload == "c5" and world == 1 and args.dropin_steps > 0:
+            dropin = time_dropin(args, net, at, u, qprime, W, dev)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, net, x_const)
+        largest = int(net.basin_sizes.max())
+        out = {
+            "metric": spec["metric"],
+            "value": value,
+            "unit": "reach-timesteps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T,
+                       "basins": int(len(net.basin_sizes)), "largest_basin": largest,
+                       "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
+                       "cut_edges_rank0": g.info.n_cut, "generations_rank0": g.info.generations,
+                       "parallelism": f"outlet basins LPT-sharded over {world} GPU(s)",
+                       "reaches_per_rank": [int(s) for s in sizes],
+                       "load_max_over_mean": float(sizes.max() / sizes.mean()),
+                       "basin_bound_speedup": float(total_reaches / max(sizes.max(), largest))},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": kc.get("bytes_per_launch"),
+                         "kernel": f"route_{dom}_kernel", "bytes_per_reach_step": kern[dom]["bytes_per_reach_step"],
+                         "valu_frac": kc.get("valu_frac"), "counters": None if cf is None else cf.get("source"),
+                         "note": "not HBM bound: VALU issue + per-tick barrier bound, see DESIGN.md section 4"},
+            "kernels": kern,
+            "step_gpu_ms": step_ms,
+            "build": lib_hash,
+            "cpu_baseline": cpu,
+        }
+        if dropin is not None:
+            out["dropin_dmc"] = dropin
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def time_dropin(args, net, at, u, qprime, W, dev):
+    """The trainer's own call path: ddr_amd.routing.dmc (torch_mc.py:144-223) on a RoutingDataclass with
+    a torch sparse-CSR adjacency, forward + backward, including setup_inputs (graph cache lookup,
+    hot start, PatternMapper) -- host work the kernel timings do not show."""
+    from types import SimpleNamespace
+
+    import scipy.sparse as sp
+
+    from ddr_amd.routing import dmc
+
+    params = SimpleNamespace(parameter_ranges=RANGES, log_space_parameters=["p_spatial"], defaults={"p_spatial": 21},
+                             attribute_minimums={"discharge": 1e-4, "slope": 1e-3, "velocity": 0.01, "depth": 0.01,
+                                                 "bottom_width": 0.01})
+    a = sp.coo_matrix((np.ones(len(net.rows), np.float32), (net.rows, net.cols)), shape=(net.n, net.n)).tocsr()
+    adj = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)), torch.from_numpy(a.indices.astype(np.int64)),
+                                  torch.from_numpy(a.data), size=(net.n, net.n))
+    rd = SimpleNamespace(adjacency_matrix=adj, length=torch.from_numpy(at.length), slope=torch.from_numpy(at.slope),
+                         x=torch.from_numpy(at.x), top_width=torch.empty(0), side_slope=torch.empty(0),
+                         outflow_idx=None, gage_catchment=None, observations=None, flow_scale=None)
+    model = dmc(SimpleNamespace(params=params), device=dev)
+    sp_params = {k: torch.from_numpy(u[k]).to(dev).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial")}
+
+    def one():
+        out = model(routing_dataclass=rd, streamflow=qprime, spatial_parameters=sp_params)["runoff"]
+        out.backward(W)
+
+    one()  # builds and caches the river graph of this adjacency
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.dropin_steps):
+        one()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.dropin_steps * 1e3
+    return {"ms_per_step": ms, "steps": args.dropin_steps,
+            "note": "dmc() forward + backward incl. setup_inputs (cached graph, hot start, PatternMapper)"}
 
 
 def block_profile(path, g, step, lib):
@@ -102,7 +417,7 @@ def block_profile(path, g, step, lib):
     bufs = [torch.zeros(16 * nb, dtype=torch.int64, device=g.device) for _ in range(2)]
     for w in (0, 1):
         lib.ddr_set_block_profile(w, ctypes.c_void_p(bufs[w].data_ptr()))
-    step(False)
+    step()
     torch.cuda.synchronize()
     for w in (0, 1):
         lib.ddr_set_block_profile(w, None)
@@ -122,159 +437,6 @@ def block_profile(path, g, step, lib):
     out["nloc"] = sizes.tolist()
     Path(path).parent.mkdir(parents=True, exist_ok=True)
     Path(path).write_text(json.dumps(out))
-
-
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reaches", type=int, default=800_000)
-    ap.add_argument("--basins", type=int, default=3000)
-    ap.add_argument("--largest", type=float, default=0.35)
-    ap.add_argument("--single-inflow", type=float, default=0.35)
-    ap.add_argument("--T", type=int, default=8760)
-    ap.add_argument("--seed", type=int, default=5)
-    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--cpu-reaches", type=int, default=40_000)
-    ap.add_argument("--cpu-T", type=int, default=720)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("nccl", device_id=dev)
-
-    t_setup = time.perf_counter()
-    net, global_n = build_rank_network(args, rank, world)
-    g = RiverGraph(net.n, net.rows, net.cols)
-    log(f"[rank {rank}] {g} built in {time.perf_counter() - t_setup:.1f}s")
-    T = args.T
-    dt = torch.float32 if args.dtype == "f32" else torch.float64
-    at = synthetic.reach_attributes(net.n, args.seed + rank)
-    u = synthetic.unit_parameters(net.n, args.seed + rank)
-    tt = lambda a: torch.from_numpy(np.asarray(a)).to(dev, dt)  # noqa: E731
-    u_n, u_q, u_p = (tt(u[k]).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial"))
-    length, slope, xs = tt(at.length), tt(np.maximum(at.slope, np.float32(1e-3))), tt(at.x)
-    qprime = synthetic.lateral_inflow_torch(net.n, T, seed=args.seed + rank, device=dev).to(dt)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    W = torch.rand((net.n, T), device=dev, dtype=dt, generator=gen)  # dL/drunoff of loss = sum(W * runoff)
-    consts = RouteConsts()
-
-    def denorm():
-        # utils.py:166-185 (torch, autograd reaches the unit-interval parameters)
-        n = u_n * (RANGES["n"][1] - RANGES["n"][0]) + RANGES["n"][0]
-        q = u_q * (RANGES["q_spatial"][1] - RANGES["q_spatial"][0]) + RANGES["q_spatial"][0]
-        lo, hi = math.log(RANGES["p_spatial"][0] + 1e-6), math.log(RANGES["p_spatial"][1])
-        p = torch.exp(u_p * (hi - lo) + lo)
-        return n, q, p
-
-    ev = {k: [] for k in ("f0", "f1", "b1")}
-    kms = {"forward": [], "backward": []}  # main routing kernels, HIP events on the launch stream
-    from ddr_amd import _lib
-
-    lib = _lib.load()
-
-    def step(record: bool):
-        for t_ in (u_n, u_q, u_p):
-            t_.grad = None
-        n, q, p = denorm()
-        if record:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        runoff, q_last, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts)
-        if record:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-        runoff.backward(W)
-        if record:
-            e2 = torch.cuda.Event(enable_timing=True)
-            e2.record()
-            ev["f0"].append(e0)
-            ev["f1"].append(e1)
-            ev["b1"].append(e2)
-            for w, key in ((0, "forward"), (1, "backward")):
-                ms = ctypes.c_float()
-                _lib.check(lib.ddr_kernel_ms(w, ctypes.byref(ms)))
-                kms[key].append(ms.value)
-        return runoff
-
-    torch.cuda.synchronize()
-    log(f"[rank {rank}] inputs resident ({torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB); warmup {args.warmup}")
-    for _ in range(args.warmup):
-        step(False)
-    _lib.check(lib.ddr_set_kernel_timing(1))
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(True)
-        log(f"[rank {rank}] step {i + 1}/{args.steps}")
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    _lib.check(lib.ddr_set_kernel_timing(0))
-    if args.block_profile and rank == 0:
-        block_profile(args.block_profile, g, step, lib)
-    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["f0"], ev["f1"])]))
-    bwd_ms = float(np.mean([a.elapsed_time(b) for a, b in zip(ev["f1"], ev["b1"])]))
-    local = torch.tensor([float(net.n)], device=dev, dtype=torch.float64)
-    tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if dist is not None:
-        dist.all_reduce(local, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    total_reaches = int(local.item())
-    elapsed = float(tmax.item())
-    value = total_reaches * (T - 1) * args.steps / elapsed
-    if rank == 0:
-        reach_steps = net.n * (T - 1)
-        kf, kb = float(np.mean(kms["forward"])), float(np.mean(kms["backward"]))
-        kern = {"forward": {"op_ms": fwd_ms, "kernel_ms": kf, "GB/s": FWD_BYTES * reach_steps / (kf * 1e-3) / 1e9},
-                "backward": {"op_ms": bwd_ms, "kernel_ms": kb, "GB/s": BWD_BYTES * reach_steps / (kb * 1e-3) / 1e9}}
-        dom = "backward" if kb >= kf else "forward"
-        achieved = kern[dom]["GB/s"]
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args)
-        out = {
-            "metric": "reach-timesteps/sec fwd+bwd (CONUS 800k reaches, 8760 h)",
-            "value": value,
-            "unit": "reach-timesteps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": args.dtype,
-            "data": "synthetic",
-            "config": {"workload": "C5: Hydrofabric-shaped synthetic forest per GPU, fwd+bwd over a water year",
-                       "reaches_per_gpu": args.reaches, "reaches_total": total_reaches, "T": T,
-                       "basins_per_gpu": args.basins, "largest_basin_frac": args.largest,
-                       "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
-                       "cut_edges_rank0": g.info.n_cut, "parallelism": f"basin-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic(f"route_{dom}_kernel", args),
-                         "kernel": f"route_{dom}_kernel",
-                         "bytes_per_reach_step": FWD_BYTES if dom == "forward" else BWD_BYTES,
-                         "note": "VALU-issue bound, not HBM bound: see DESIGN.md section 4"},
-            "kernels": kern,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

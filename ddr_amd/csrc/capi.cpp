@@ -500,6 +500,9 @@ ddr_status ddr_device_info(int32_t* n_cu, int32_t* max_resident) {
 }
 
 const char* ddr_last_error(void) { return ddr::last_error_cstr(); }
-const char* ddr_version(void) { return "ddr_mc 0.1.0 (gfx950)"; }
+#ifndef DDR_SOURCE_HASH
+#define DDR_SOURCE_HASH "unknown"
+#endif
+const char* ddr_version(void) { return "ddr_mc 0.2.0 (gfx950) src " DDR_SOURCE_HASH; }
 
 }  // extern "C"

@@ -167,6 +167,17 @@ class RiverGraph:
         src[diag_pos] = 0
         return crow_a, col_a, src
 
+    def pattern_mapper_tensors(self, device=None):
+        """:meth:`pattern_mapper_layout` as int64 tensors on ``device``, cached per device."""
+        import torch
+
+        key = str(torch.device(device)) if device is not None else "cpu"
+        cache = self.__dict__.setdefault("_pm_cache", {})
+        if key not in cache:
+            crow, col, src = (torch.from_numpy(v) for v in self.pattern_mapper_layout())
+            cache[key] = tuple(t.to(device) if device is not None else t for t in (crow, col, src))
+        return cache[key]
+
     def structure(self) -> dict[str, np.ndarray]:
         out = {k: np.zeros(self.n, dtype=np.int64) for k in ("down", "dist", "basin", "block")}
         _lib.check(_lib.load().ddr_graph_structure(self._handle, *(out[k].ctypes.data for k in

@@ -52,18 +52,28 @@ class PatternMapper:
             col = A.col_indices().to(torch.int64)
             src = (A.values().to(torch.float64).round().to(torch.int64) - offset)
         else:
-            crow, col, src = graph.pattern_mapper_layout()
-            crow, col, src = (torch.from_numpy(v) for v in (crow, col, src))
+            # the graph caches its layout (per device): one build per adjacency, not per forward
+            crow, col, src = graph.pattern_mapper_tensors(device)
         self.crow_indices = crow.to(device) if device is not None else crow
         self.col_indices = col.to(device) if device is not None else col
         self.src_index = src.to(self.crow_indices.device)
-        n_vals = len(src)
-        cidx = torch.arange(0, n_vals, dtype=torch.int64) + indShift
-        indices = torch.stack((src.cpu(), cidx), 0)
-        ones = torch.ones(n_vals)
-        M_coo = torch.sparse_coo_tensor(indices, ones, size=(matrix_dim, n_vals))
-        self.M_csr = M_coo.to_sparse_csr().to(self.crow_indices.device)
+        self._matrix_dim = matrix_dim
+        self._ind_shift = indShift
+        self._M_csr = None
         self.graph = graph
+
+    @property
+    def M_csr(self) -> torch.Tensor:
+        """The (N, nnz) selection matrix of the reference's ``map`` (utils.py:83-102), built on first
+        use: the fused routing path never needs it (``map`` here is a gather)."""
+        if self._M_csr is None:
+            src = self.src_index.cpu()
+            n_vals = len(src)
+            cidx = torch.arange(0, n_vals, dtype=torch.int64) + self._ind_shift
+            M_coo = torch.sparse_coo_tensor(torch.stack((src, cidx), 0), torch.ones(n_vals),
+                                            size=(self._matrix_dim, n_vals))
+            self._M_csr = M_coo.to_sparse_csr().to(self.crow_indices.device)
+        return self._M_csr
 
     def map(self, datvec: torch.Tensor) -> torch.Tensor:
         """A_values[k] = datvec[src(k)] (utils.py:89-102); differentiable gather."""

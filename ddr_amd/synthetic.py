@@ -186,13 +186,19 @@ def lateral_inflow(n: int, T: int, seed: int = 0, t0: int = 0) -> np.ndarray:
     return (a[None, :] * (1.0 + 0.5 * np.sin(2 * math.pi * t / 24.0 + phi[None, :])) * season).astype(np.float32)
 
 
-def lateral_inflow_torch(n: int, T: int, seed: int = 0, device="cuda", chunk: int = 256):
-    """Same law as ``lateral_inflow`` generated on the device in time chunks (large T·N)."""
+def lateral_inflow_torch(n: int, T: int, seed: int = 0, device="cuda", chunk: int = 256, ids=None):
+    """Same law as ``lateral_inflow`` generated on the device in time chunks (large T·N).  With ``ids``
+    only those columns of the n-reach field (a rank's shard of a global network)."""
     import torch
 
     rng = np.random.default_rng(seed + 2000)
-    a = torch.from_numpy(rng.lognormal(math.log(0.5), 1.0, n).astype(np.float32)).to(device)
-    phi = torch.from_numpy(rng.uniform(0, 2 * math.pi, n).astype(np.float32)).to(device)
+    a = rng.lognormal(math.log(0.5), 1.0, n).astype(np.float32)
+    phi = rng.uniform(0, 2 * math.pi, n).astype(np.float32)
+    if ids is not None:
+        a, phi = a[ids], phi[ids]
+        n = len(ids)
+    a = torch.from_numpy(a).to(device)
+    phi = torch.from_numpy(phi).to(device)
     out = torch.empty((T, n), dtype=torch.float32, device=device)
     for s in range(0, T, chunk):
         e = min(T, s + chunk)
@@ -218,3 +224,10 @@ def network_stats(net: SyntheticNetwork) -> dict:
     indeg = np.bincount(net.rows, minlength=n)
     return dict(n=n, edges=len(net.rows), basins=len(net.basin_sizes), max_depth=int(dist.max()) + 1,
                 largest_basin=int(net.basin_sizes.max()), single_inflow_frac=float((indeg == 1).mean()))
+
+
+def reach_features(n: int, n_attr: int = 10, seed: int = 0) -> np.ndarray:
+    """Normalised catchment attributes (N, n_attr) for a parameter network (the reference feeds the KAN
+    ``routing_dataclass.normalized_spatial_attributes``, scripts/train.py:71)."""
+    rng = np.random.default_rng(seed + 5000)
+    return rng.standard_normal((n, n_attr)).astype(np.float32)
