@@ -44,7 +44,7 @@ sys.path.insert(0, str(ROOT))
 from ddr_amd import _lib, synthetic  # noqa: E402
 from ddr_amd.graph import RiverGraph  # noqa: E402
 from ddr_amd.ops import DailyWindow, GaugeMap, RouteConsts, route  # noqa: E402
-from ddr_amd.partition import extract_basins, shard_basins  # noqa: E402
+from ddr_amd.distributed import shard_network  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
 RANGES = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
@@ -78,15 +78,7 @@ def global_network(args):
     return synthetic.hack_basin(5000, seed=2), None
 
 
-def shard(net, rank, world):
-    """Reaches (global ids, ascending) and sub-network of the basins LPT-assigned to this rank."""
-    starts = np.concatenate([[0], np.cumsum(net.basin_sizes)[:-1]])
-    mine = np.sort(shard_basins(net.basin_sizes, world)[rank])
-    keep = np.zeros(net.n, bool)
-    for b in mine:
-        keep[starts[b]:starts[b] + net.basin_sizes[b]] = True
-    n_sub, rows, cols, ids = extract_basins(net.n, net.rows, net.cols, keep)
-    return n_sub, rows, cols, ids, mine
+
 
 
 class ParamNet(torch.nn.Module):
@@ -192,21 +184,29 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # rehearsal knobs (a 1-GPU box): DDR_BENCH_SAME_DEVICE=1 puts every rank on device 0 and
+    # DDR_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one device
+    local_dev = 0 if os.environ.get("DDR_BENCH_SAME_DEVICE") == "1" else local_rank
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("DDR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     t_setup = time.perf_counter()
     net, x_const = global_network(args)
     args.reaches_total = net.n
-    n_loc, rows, cols, ids, my_basins = shard(net, rank, world) if world > 1 else (
-        net.n, net.rows, net.cols, np.arange(net.n), np.arange(len(net.basin_sizes)))
+    # this rank's outlet basins (LPT by reach count, distributed.shard_network; all of them at N = 1)
+    n_loc, rows, cols, ids = shard_network(net.n, net.rows, net.cols, rank, world) if world > 1 else (
+        net.n, net.rows, net.cols, np.arange(net.n))
     g = RiverGraph(n_loc, rows, cols, steps_hint=T)
-    log(f"[rank {rank}] {g} ({len(my_basins)} basins) built in {time.perf_counter() - t_setup:.1f}s")
+    log(f"[rank {rank}] {g} built in {time.perf_counter() - t_setup:.1f}s")
     at = synthetic.reach_attributes(net.n, 11, x_const=x_const)
     u = synthetic.unit_parameters(net.n, 11)
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a)[ids])).to(dev)  # noqa: E731
@@ -236,12 +236,14 @@ def main():
         feats = tt(synthetic.reach_features(net.n, seed=11))
         model = ParamNet().to(dev)
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-        outlets = np.flatnonzero(np.asarray(synthetic.SyntheticNetwork(n_loc, rows, cols, np.array([n_loc])).down) < 0)
+        # one gauge per subnetwork outlet; observations indexed by the gauge's global number
+        outlets_global = np.flatnonzero(net.down < 0)
+        outlets = np.flatnonzero(np.isin(ids, outlets_global))
         gz = GaugeMap.build([np.array([o]) for o in outlets], n_loc, dev)
         window = DailyWindow.for_training(T, args.tau)
-        G_global = len(net.basin_sizes)
+        G_global = len(outlets_global)
         obs = torch.from_numpy(np.random.default_rng(100).lognormal(np.log(5.0), 1.0, (G_global, window.D))
-                               .astype(np.float32)[my_basins]).to(dev)
+                               .astype(np.float32)[np.searchsorted(outlets_global, ids[outlets])]).to(dev)
         wd = args.warmup_days
 
         def step():

@@ -60,14 +60,32 @@ def allreduce_gradients(params, op_average: bool = False) -> None:
 
 
 def gather_rows(local: torch.Tensor, global_index: torch.Tensor, n_global: int) -> torch.Tensor:
-    """Assemble a (n_global, ...) tensor from every rank's rows (e.g. gauge discharge (G_r, T))."""
+    """Assemble a (n_global, ...) tensor from every rank's rows (e.g. gauge discharge (G_r, T) or the
+    daily objective series (G_r, D)) on every rank.
+
+    One all-gather of the row indices and one of the rows, each padded to the largest shard: the
+    traffic is world x max_rows, not the world x n_global of an all-reduce over a zero-padded copy."""
     import torch.distributed as dist
 
+    out = local.new_zeros((n_global,) + tuple(local.shape[1:]))
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        out = local.new_zeros((n_global,) + tuple(local.shape[1:]))
         out[global_index] = local
         return out
-    out = local.new_zeros((n_global,) + tuple(local.shape[1:]))
-    out[global_index] = local
-    dist.all_reduce(out, op=dist.ReduceOp.SUM)
+    world = dist.get_world_size()
+    idx = global_index.to(device=local.device, dtype=torch.int64)
+    cnt = torch.tensor([idx.numel()], device=local.device, dtype=torch.int64)
+    counts = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    m = int(max(int(c.item()) for c in counts))
+    pad_idx = torch.full((m,), -1, device=local.device, dtype=torch.int64)
+    pad_idx[:idx.numel()] = idx
+    pad_rows = local.new_zeros((m,) + tuple(local.shape[1:]))
+    pad_rows[:idx.numel()] = local
+    all_idx = [torch.empty_like(pad_idx) for _ in range(world)]
+    all_rows = [torch.empty_like(pad_rows) for _ in range(world)]
+    dist.all_gather(all_idx, pad_idx)
+    dist.all_gather(all_rows, pad_rows)
+    for i_, r_ in zip(all_idx, all_rows):
+        keep = i_ >= 0
+        out[i_[keep]] = r_[keep]
     return out

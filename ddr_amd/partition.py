@@ -14,16 +14,17 @@ import numpy as np
 
 
 def basin_labels(n: int, rows: np.ndarray, cols: np.ndarray) -> np.ndarray:
-    """Outlet reach id of every reach (rows = downstream, cols = upstream, lower triangular)."""
-    down = np.full(n, -1, dtype=np.int64)
-    down[np.asarray(cols, dtype=np.int64)] = np.asarray(rows, dtype=np.int64)
+    """Outlet reach id of every reach (rows = downstream, cols = upstream, lower triangular).
+
+    Pointer jumping: every reach points at its downstream reach (an outlet at itself) and the pointers
+    are squared until they stop moving -- ceil(log2(depth)) vectorised passes."""
     lab = np.arange(n, dtype=np.int64)
-    # downstream-first sweep (down[i] > i for a topologically ordered network)
-    for i in range(n - 1, -1, -1):
-        d = down[i]
-        if d >= 0:
-            lab[i] = lab[d]
-    return lab
+    lab[np.asarray(cols, dtype=np.int64)] = np.asarray(rows, dtype=np.int64)
+    while True:
+        nxt = lab[lab]
+        if np.array_equal(nxt, lab):
+            return lab
+        lab = nxt
 
 
 def lpt_assign(costs, n_bins: int, tiebreak=None) -> np.ndarray:

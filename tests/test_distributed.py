@@ -118,3 +118,94 @@ def test_shard_network_covers_every_reach(world):
             assert np.all(rs > cs)  # still topologically ordered
         seen.append(ids)
     np.testing.assert_array_equal(np.sort(np.concatenate(seen)), np.arange(net.n))
+
+
+# ---- C3 training objective over ranks: gauges sharded with their basins ---------------------------
+
+T_DAILY = 96  # 4 days: window [13, 88), 3 pooled days
+
+
+def _objective_grad(rows, cols, n, ids, case, feats, weight, outlets_global, obs, g_global, warmup=1):
+    """This rank's share of the global mean daily L1 (train.py:78-97, one gauge per basin outlet) and
+    its gradient w.r.t. the parameter-network weight; plus its (G_local, D) daily series."""
+    from oracle import mc_oracle as O
+
+    w = torch.tensor(weight, requires_grad=True)
+    u = torch.sigmoid(torch.from_numpy(feats[ids]) @ w)
+    uu = u.detach().numpy().astype(np.float32)
+    rngs = PARAMS_DEFAULT["parameter_ranges"]
+    r = O.Reaches(O.denormalize(uu[:, 0], rngs["n"]), O.denormalize(uu[:, 1], rngs["q_spatial"]),
+                  O.denormalize(uu[:, 2], rngs["p_spatial"], True), case.length[ids],
+                  np.maximum(case.slope[ids], np.float32(1e-3)), case.x[ids])
+    net = O.Network.from_coo(n, rows, cols)
+    qp = case.qprime[:, ids]
+    local_out = np.flatnonzero(np.isin(ids, outlets_global))  # local gauge reaches (ascending)
+    gidx = np.searchsorted(outlets_global, ids[local_out])    # their global gauge numbers
+    res = O.route(net, r, qp, dtype=np.float64, outflow_idx=[np.array([o]) for o in local_out])
+    loss_l, daily, gh = O.daily_l1_objective(res["runoff"], obs[gidx], tau=3, warmup=warmup)
+    share = len(local_out) / g_global  # local mean -> this rank's part of the global mean
+    Wg = np.zeros((n, T_DAILY))
+    Wg[local_out] = gh * share
+    res64 = O.route(net, r, qp, dtype=np.float64)
+    bw = O.route_backward(net, r, qp, res64["x"], Wg)
+    g = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], uu[:, 0], uu[:, 1], uu[:, 2], rngs)
+    u.backward(torch.from_numpy(np.stack([g["n"], g["q_spatial"], g["p_spatial"]], 1).astype(np.float32)))
+    return w.grad.numpy(), loss_l * share, daily, gidx
+
+
+def _objective_problem():
+    from ddr_amd import synthetic
+
+    net = synthetic.forest(synthetic.loguniform_sizes(10, 20, 300, 4), seed=6)
+    case = synthetic_case(net, T_DAILY, 6)
+    feats = np.random.default_rng(7).normal(size=(net.n, 4)).astype(np.float32)
+    outlets = np.flatnonzero(net.down < 0)
+    obs = np.random.default_rng(8).lognormal(0.0, 1.0, (len(outlets), 3)).astype(np.float32)
+    weight = np.random.default_rng(10).normal(size=(4, 3)).astype(np.float32) * 0.3
+    return net, case, feats, outlets, obs, weight
+
+
+def _objective_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from ddr_amd.distributed import allreduce_gradients, gather_rows, shard_network
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    net, case, feats, outlets, obs, weight = _objective_problem()
+    ns, rs, cs, ids = shard_network(net.n, net.rows, net.cols, rank, world)
+    grad, loss, daily, gidx = _objective_grad(rs, cs, ns, ids, case, feats, weight, outlets, obs, len(outlets))
+    p = torch.nn.Parameter(torch.zeros(4, 3))
+    p.grad = torch.from_numpy(grad)
+    allreduce_gradients([p])
+    lt = torch.tensor([loss], dtype=torch.float64)
+    dist.all_reduce(lt)
+    full_daily = gather_rows(torch.from_numpy(daily.astype(np.float64)), torch.from_numpy(gidx), len(outlets))
+    out[rank] = (p.grad.numpy().copy(), float(lt), full_daily.numpy())
+    dist.destroy_process_group()
+
+
+def test_two_rank_c3_objective_allreduce_and_gather():
+    """The multi-GPU C3 step at world size 2 (gloo): gauges follow their basins, each rank's L1 is its
+    share of the global mean, the all-reduced gradient equals the single-process one and gather_rows
+    reassembles the (G, D) daily series in global gauge order on every rank."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    world = 2
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    procs = [ctx.Process(target=_objective_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    net, case, feats, outlets, obs, weight = _objective_problem()
+    full_grad, full_loss, full_daily, _ = _objective_grad(net.rows, net.cols, net.n, np.arange(net.n), case, feats,
+                                                         weight, outlets, obs, len(outlets))
+    for r in range(world):
+        g, loss, daily = out[r]
+        np.testing.assert_allclose(g, full_grad, rtol=2e-4, atol=1e-6)
+        assert abs(loss - full_loss) <= 1e-9 * abs(full_loss)
+        np.testing.assert_allclose(daily, full_daily, rtol=1e-8)  # SciPy solves of sub- vs whole network

@@ -1,0 +1,63 @@
+"""Turn a tools/pmc.sh run into profiles/counters/<workload>.json, keyed to the library build.
+
+bench.py reports roofline.traffic / valu_frac from this file only while the loaded library's source
+hash (ddr_version) and the workload configuration match.
+
+HBM bytes per dispatch = 2 x FETCH_SIZE + WRITE_SIZE (KiB; the gfx950 FETCH_SIZE halving of wide
+streaming reads, MI355X_MICROARCH.md "HBM").  VALU issue fraction = SQ_INSTS_VALU x 2 cycles (wave64
+on a SIMD-32) / (SIMD count x cycles the kernel ran), the cycles from GRBM_GUI_ACTIVE / 8 XCDs.
+
+Usage: python tools/pmc_to_json.py gpurun_out/TAG/pmc WORKLOAD BUILD_HASH T REACHES [SOURCE_NAME]
+"""
+import glob
+import json
+import sqlite3
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+root, workload, build, T, reaches = sys.argv[1:6]
+source = sys.argv[6] if len(sys.argv) > 6 else root
+vals = defaultdict(dict)
+dbs = sorted(glob.glob(f"{root}/p*/run_results.db"))
+for db in dbs:
+    c = sqlite3.connect(db)
+    q = ("select kernel_name, counter_name, sum(value), count(distinct dispatch_id) from counters_collection "
+         "group by kernel_name, counter_name")
+    for k, cn, v, nd in c.execute(q):
+        vals[k][cn] = v / max(nd, 1)
+if not dbs:  # the databases were pruned: read tools/pmc_report.py's summary instead
+    cur = None
+    for line in Path(root, "report.txt").read_text().splitlines():
+        if not line.startswith(" "):
+            cur = line.strip()
+        elif cur is not None:
+            parts = line.split()
+            if len(parts) == 2 and parts[0].isupper():
+                try:
+                    vals[cur][parts[0]] = float(parts[1])
+                except ValueError:
+                    pass
+SIMDS = 256 * 4
+kernels = {}
+for k, d in vals.items():
+    name = k.split("(")[0].split("::")[-1].split("<")[0]
+    if not any(s in name for s in ("route_", "gather_", "gauge_", "geometry_")):
+        continue
+    e = {}
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+        e["bytes_per_launch"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+    if "SQ_INSTS_VALU" in d and d.get("GRBM_GUI_ACTIVE"):
+        e["valu_frac"] = 2 * d["SQ_INSTS_VALU"] / (SIMDS * d["GRBM_GUI_ACTIVE"] / 8)
+    if "SQ_WAVE_CYCLES" in d:
+        w = d["SQ_WAVE_CYCLES"]
+        e["wave_cycle_split"] = {"active": d.get("SQ_ACTIVE_INST_ANY", 0) / w, "parked": d.get("SQ_WAIT_ANY", 0) / w,
+                                 "issue_stall": d.get("SQ_WAIT_INST_ANY", 0) / w}
+    e["counters"] = d
+    kernels[name] = e
+out = {"workload": workload, "build": build, "T": int(T), "reaches": int(reaches), "source": source,
+       "kernels": kernels}
+dst = Path(__file__).resolve().parents[1] / "profiles" / "counters" / f"{workload}.json"
+dst.parent.mkdir(parents=True, exist_ok=True)
+dst.write_text(json.dumps(out, indent=1))
+print(dst, {k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()})
