@@ -176,6 +176,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dropin-steps", type=int, default=2, help="C5, 1 GPU: also time the drop-in dmc() path")
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
+    ap.add_argument("--fast-math", action="store_true",
+                    help="forward coefficients in hardware-approximate fp32 math (route(fast_math=True))")
     args = ap.parse_args()
     spec = WORKLOADS[args.workload]
     T = args.T or spec["T"]
@@ -227,7 +229,7 @@ def main():
             for t_ in (u_n, u_q, u_p):
                 t_.grad = None
             n, q, p = denorm(u_n, u_q, u_p)
-            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts)
+            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, fast_math=args.fast_math)
             runoff.backward(W)
 
     elif args.workload == "c3":
@@ -250,7 +252,8 @@ def main():
             opt.zero_grad(set_to_none=True)
             un = model(feats)
             n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
-            daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts)
+            daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
+                                   fast_math=args.fast_math)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
             loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
             loss.backward()
@@ -267,7 +270,7 @@ def main():
             with torch.no_grad():
                 if args.workload == "c4":  # first: the kernel timer reports the last forward launch
                     geometry_statistics_from_inflow(g, qprime[::24][:365], n, p, q, slope)
-                route(g, qprime, n, q, p, length, slope, xs, consts=consts, save=False)
+                route(g, qprime, n, q, p, length, slope, xs, consts=consts, save=False, fast_math=args.fast_math)
 
     ev = []
     kms = {"forward": [], "backward": []}  # main routing kernels, HIP events on the launch stream
@@ -352,6 +355,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T,
+                       "forward_math": "fast (hardware rcp/log/exp fp32)" if args.fast_math else "exact (reference op order)",
                        "basins": int(len(net.basin_sizes)), "largest_basin": largest,
                        "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
                        "cut_edges_rank0": g.info.n_cut, "generations_rank0": g.info.generations,
@@ -416,7 +420,8 @@ def time_dropin(args, net, at, u, qprime, W, dev):
 def block_profile(path, g, step, lib):
     """One extra step with the per-workgroup profile on: start/end/import-wait per block (µs)."""
     nb = g.info.n_blocks
-    bufs = [torch.zeros(16 * nb, dtype=torch.int64, device=g.device) for _ in range(2)]
+    # 16 words per block, then (phase-profile builds, -DDDR_PHASE_PROF=1) 8 phase counters per wave
+    bufs = [torch.zeros(16 * nb + nb * 16 * 8, dtype=torch.int64, device=g.device) for _ in range(2)]
     for w in (0, 1):
         lib.ddr_set_block_profile(w, ctypes.c_void_p(bufs[w].data_ptr()))
     step()
@@ -427,7 +432,15 @@ def block_profile(path, g, step, lib):
     sizes = np.bincount(s["block"], minlength=nb)
     out = {}
     for w, key in ((0, "forward"), (1, "backward")):
-        p = bufs[w].view(nb, 16).cpu().numpy()
+        allw = bufs[w].cpu().numpy()
+        p = allw[:16 * nb].reshape(nb, 16)
+        ph = allw[16 * nb:].reshape(nb * 16, 8)
+        ph = ph[ph.sum(1) > 0]
+        if len(ph):
+            tot = ph.sum(0).astype(np.float64)
+            out[key + "_phase_frac"] = (tot / tot.sum()).tolist()
+            log(f"[profile] {key} phases (cycle share over {len(ph)} waves): "
+                + " ".join(f"{f:.3f}" for f in tot / tot.sum()))
         t0 = p[:, 0].min()
         out[key] = {"start_us": ((p[:, 0] - t0) / 100.0).tolist(), "end_us": ((p[:, 1] - t0) / 100.0).tolist(),
                     "wait_us": (p[:, 2] / 100.0).tolist(), "hwid": (p[:, 3] & 0xFFFFFFFF).tolist(),

@@ -36,6 +36,7 @@ DDR_FWD_SAVE_X = 1
 DDR_FWD_CARRY = 2
 DDR_FWD_NO_RUNOFF = 4
 DDR_FWD_ACCUMULATE = 8
+DDR_FWD_FAST_MATH = 16
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 

@@ -41,6 +41,7 @@ struct Piece {
   int64_t size = 0;
   int64_t height = 0;
   int64_t dmax = 0;  // max in-piece dist including virtual inflows
+  int64_t xl = 0;    // confluence-list entries (reaches with more than two inflows, route.hip)
 };
 
 }  // namespace
@@ -187,6 +188,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       }
       Piece& P = pieces[piece[i]];
       P.size++;
+      if (cnt[i + 1] - cnt[i] > 2) P.xl += cnt[i + 1] - cnt[i];
       P.dmax = std::max(P.dmax, dloc_piece[i]);
     }
     // virtual inflows deepen the consuming piece by one tick; piece heights (children first:
@@ -219,8 +221,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       const int64_t r = pieces[p].root;
       const double L = (double)(ht[r] + g->dist[r] + kChunk * (hops_down[p] + pieces[p].height));
       fac[p] = weighted ? (steps + L) / steps : 1.0;
-      wsum += (double)pieces[p].size * fac[p];
     }
+    for (size_t p = 0; p < pieces.size(); ++p) wsum += (double)pieces[p].size * fac[p];
     // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
     // Pieces are taken by factor (descending) so blocks gather pieces of similar factor; capw is
     // the smallest (1 % steps) that packs into the target number of workgroups.
@@ -265,24 +267,27 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     {
       // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if two
       // workgroups would no longer fit on a CU
-      std::vector<int64_t> bv(nblocks, 0), bc(nblocks, 0);
+      std::vector<int64_t> bv(nblocks, 0), bc(nblocks, 0), bx(nblocks, 0);
       for (size_t p = 0; p < pieces.size(); ++p) {
+        bx[block_of_piece[p]] += pieces[p].xl;
         const int64_t d = g->down[pieces[p].root];
         if (d >= 0) {
           bv[block_of_piece[piece[d]]]++;
           bc[block_of_piece[p]]++;
         }
       }
-      int64_t ms = 0, mv = 0, mc = 0;
+      int64_t ms = 0, mv = 0, mc = 0, mx = 0;
       for (int64_t b = 0; b < nblocks; ++b) {
         ms = std::max(ms, load[b] + bv[b]);
         mv = std::max(mv, bv[b]);
         mc = std::max(mc, bc[b]);
+        mx = std::max(mx, bx[b]);
       }
-      const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, false, 4),
-                                   route_lds_bytes(route_slot_stride((int)ms), mc, true, 4));
-      if (getenv("DDR_DEBUG_PART")) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld lds %zu\n", (long)ms, (long)mv, (long)mc, need);
-      if (need > kLdsBudget) {
+      const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4),
+                                   route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
+      if (getenv("DDR_DEBUG_PART"))
+        fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
+      if (need > kLdsBudget || mx >= kMaxConfluenceList) {
         if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
         hard_cap -= std::max<int64_t>(1, hard_cap / 32);
         cap = std::min(cap, hard_cap);
@@ -321,23 +326,30 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     for (int64_t i = 0; i < n; ++i) offv[i] = bdmax[g->block_of[i]] - dloc_piece[i];
     // internal order: blocks contiguous; inside a block by (tick offset, reference index)
     std::vector<int64_t> pos(n), local(n);
-    std::vector<int32_t> ref(n), offs(n), upb(n), upc(n), dl(n), cut(n, -1), uplist;
+    std::vector<int32_t> ref(n), offs(n), upb(n), upc(n), dl(n), cut(n, -1), xoff(n, -1), uplist;
     std::vector<int32_t> v_edge, v_off, v_dloc, cout_loc;
     std::vector<int64_t> edge_id(n, -1);
+    // Cut edges are numbered in (block, local position) order, i.e. by their index in cout_loc: the
+    // forward kernel derives a cut reach's granule row from B.cout0 + its rank among the block's
+    // cut reaches (route.hip), with no table load in the tick.
+    for (int64_t b = 0; b < nblocks; ++b)
+      std::stable_sort(members[b].begin(), members[b].end(), [&](int64_t a, int64_t c) {
+        if (offv[a] != offv[c]) return offv[a] < offv[c];
+        return a < c;
+      });
     int64_t eid = 0;
-    for (int64_t i = 0; i < n; ++i)
-      if (is_root[i] && g->down[i] >= 0) edge_id[i] = eid++;
+    for (int64_t b = 0; b < nblocks; ++b)
+      for (int64_t i : members[b])
+        if (g->down[i] >= 0 && g->block_of[g->down[i]] != b) edge_id[i] = eid++;
+    g->n_cut = eid;  // inter-workgroup edges (pieces packed into one block hand off in LDS)
+    std::vector<int32_t> xlist;
     g->blocks.assign(nblocks, BlockDesc{});
     int64_t p0 = 0, pre_dn = 0;
-    g->max_slots = g->max_virt = g->max_cout = 0;
+    g->max_slots = g->max_virt = g->max_cout = g->max_xl = 0;
     g->max_block_depth = 0;
     int64_t max_load = 0;
     for (int64_t b = 0; b < nblocks; ++b) {
       auto& m = members[b];
-      std::stable_sort(m.begin(), m.end(), [&](int64_t a, int64_t c) {
-        if (offv[a] != offv[c]) return offv[a] < offv[c];
-        return a < c;
-      });
       for (size_t r = 0; r < m.size(); ++r) {
         pos[m[r]] = p0 + (int64_t)r;
         local[m[r]] = (int64_t)r;
@@ -349,6 +361,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       B.cout0 = (int32_t)cout_loc.size();
       B.dmax = (int32_t)bdmax[b];
       B.pre_dn = pre_dn;
+      B.xl0 = (int32_t)xlist.size();
       max_load = std::max<int64_t>(max_load, (int64_t)m.size());
       for (size_t r = 0; r < m.size(); ++r) {
         int64_t i = m[r];
@@ -369,6 +382,12 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
             v_dloc.push_back((int32_t)r);
           }
         }
+        if (upc[P] > 2) {
+          // confluence list: [c, u1, ..., u_{c-1}] at xoff (block-local), see route.hip pack_up
+          xoff[P] = (int32_t)(xlist.size() - B.xl0);
+          xlist.push_back(upc[P]);
+          for (int32_t k = 1; k < upc[P]; ++k) xlist.push_back(uplist[upb[P] + k]);
+        }
         int64_t d = g->down[i];
         dl[P] = (d >= 0 && g->block_of[d] == b) ? -2 : -1;  // resolved below (local of d)
         if (d >= 0 && g->block_of[d] != b) {
@@ -378,6 +397,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       }
       B.nvirt = (int32_t)(v_edge.size() - B.virt0);
       B.ncout = (int32_t)(cout_loc.size() - B.cout0);
+      B.nxl = (int32_t)(xlist.size() - B.xl0);
+      g->max_xl = std::max<int>(g->max_xl, B.nxl);
       g->max_slots = std::max<int>(g->max_slots, B.nloc + B.nvirt);
       g->max_virt = std::max<int>(g->max_virt, B.nvirt);
       g->max_cout = std::max<int>(g->max_cout, B.ncout);
@@ -408,6 +429,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     if ((st = upload(g.get(), &D.dloc, dl))) return st;
     if ((st = upload(g.get(), &D.cut, cut))) return st;
     if ((st = upload(g.get(), &D.uplist, uplist))) return st;
+    if ((st = upload(g.get(), &D.xoff, xoff))) return st;
+    if ((st = upload(g.get(), &D.xlist, xlist))) return st;
     if ((st = upload(g.get(), &D.v_edge, v_edge))) return st;
     if ((st = upload(g.get(), &D.v_off, v_off))) return st;
     if ((st = upload(g.get(), &D.v_dloc, v_dloc))) return st;

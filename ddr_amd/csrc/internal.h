@@ -45,11 +45,21 @@ __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_sl
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
 //   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64
 //   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunk][2] (R)
-// (after the math tables of fastmath.h, which occupy the first kMathTabBytes)
+//             | owner words
+// and then the block's confluence lists (after the math tables of fastmath.h, which occupy the first
+// kMathTabBytes)
 constexpr size_t kMathTabBytes = 3072;
-__host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nring, bool backward, size_t rsize) {
+// Confluence lists (reaches with more than two inflows) of a block, in LDS after the ring: at most
+// kMaxConfluenceList int32 entries per block (13-bit offsets in the packed upstream word).
+constexpr int kMaxConfluenceList = 8191;
+__host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nvirt, size_t ncout, size_t nxl, bool backward,
+                                                  size_t rsize) {
   const size_t base = backward ? slots * 9 * rsize : slots * (8 + 6 * rsize);
-  return kMathTabBytes + align16(base) + nring * kChunk * (backward ? 2 * rsize : 8);
+  const size_t ring = backward ? ncout * kChunk * 2 * rsize : nvirt * kChunk * 8;
+  // backward: per hand-off owner thread (tid < max(nvirt, ncout)) its virtual's downstream slot and
+  // its cut-out's tick offset
+  const size_t own = backward ? align16(4 * (nvirt > ncout ? nvirt : ncout)) : 0;
+  return kMathTabBytes + align16(base) + align16(ring) + own + nxl * 4;
 }
 
 // One workgroup's slice of the schedule.  Reaches of a block occupy internal positions
@@ -62,8 +72,10 @@ struct BlockDesc {
   int32_t cout0;   // index into cout_loc (reaches whose downstream lives in another block)
   int32_t ncout;
   int32_t dmax;    // ticks = T + dmax
-  int32_t pad;
+  int32_t nxl;     // confluence-list entries (LDS copy of xlist[xl0, xl0 + nxl))
   int64_t pre_dn;  // sum over earlier blocks of dmax * nloc (x_save base = T*pos0 + pre_dn)
+  int32_t xl0;
+  int32_t pad;
 };
 
 // Device-side schedule (structure of arrays, indexed by internal position unless noted).
@@ -76,6 +88,8 @@ struct DevSchedule {
   int32_t* dloc = nullptr;     // downstream local index in the same block, -1 otherwise
   int32_t* cut = nullptr;      // cut-edge id if the downstream is in another block, -1 otherwise
   int32_t* uplist = nullptr;   // local index (< nloc) or nloc + virtual index
+  int32_t* xoff = nullptr;     // block-local confluence-list offset (upc > 2), else -1
+  int32_t* xlist = nullptr;    // per block: for each confluence [c, u1, ..., u_{c-1}]
   int32_t* v_edge = nullptr;   // per virtual: cut-edge id
   int32_t* v_off = nullptr;    // per virtual: tick offset (= off(consumer) - 1)
   int32_t* v_dloc = nullptr;   // per virtual: consumer local index
@@ -94,6 +108,7 @@ struct Graph {
   int bs = kBlockThreads, kr = 1;
   int max_slots = 0;     // max over blocks of nloc + nvirt
   int max_virt = 0, max_cout = 0;
+  int max_xl = 0;        // max over blocks of nxl
   int device = 0;
   std::vector<BlockDesc> blocks;
   int64_t sum_dn = 0;    // sum over blocks of dmax * nloc

@@ -267,6 +267,36 @@ __device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], c
   DDR_FOR_NP o[h].c4 = b[h];
 }
 
+// Hardware-approximate fp32 form of coefficients_np (v_rcp / v_log / v_exp / v_rsq, the operation
+// set of the adjoint's recompute, adjoint_step_fast): ~1e-6 relative per coefficient.
+__device__ __forceinline__ PhysOut<float> coefficients_fast(const ReachStatic<float>& s, float Q, const Consts<float>& c) {
+  const float qe = s.qe;
+  const float ratio = ((Q * s.n) * (qe + 1.0f)) * __builtin_amdgcn_rcpf(s.dd);
+  const float pw = __builtin_amdgcn_exp2f(s.expo * __builtin_amdgcn_logf(ratio));
+  const float depth = rmax(pw, c.dlb);
+  const float dq = __builtin_amdgcn_exp2f(qe * __builtin_amdgcn_logf(depth));
+  PhysOut<float> o;
+  o.tw = s.p * dq;
+  const float td = depth + depth;
+  const float ssr = (o.tw * qe) * __builtin_amdgcn_rcpf(td);
+  o.ss = rclamp(ssr, c.sslb, c.ssub);
+  const float bw = rmax(o.tw - (o.ss + o.ss) * depth, c.bwlb);
+  const float area = ((o.tw + bw) * depth) * 0.5f;
+  const float u = fmaf(o.ss, o.ss, 1.0f);
+  const float wp = fmaf(td, u * __builtin_amdgcn_rsqf(u), bw);
+  const float Rh = area * __builtin_amdgcn_rcpf(wp);
+  const float r23 = __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(Rh) * (2.0f / 3.0f));
+  const float cel = rclamp((s.inv_n * r23) * s.sqrtS, c.vlb, c.vub) * (5.0f / 3.0f);
+  const float twok = 2.0f * (s.L * __builtin_amdgcn_rcpf(cel));
+  const float rden = __builtin_amdgcn_rcpf(fmaf(twok, 1.0f - s.X, c.dt));
+  const float tX = twok * s.X;
+  o.c1 = (c.dt - tX) * rden;
+  o.c2 = (c.dt + tX) * rden;
+  o.c4 = (2.0f * c.dt) * rden;
+  o.c3 = 1.0f - o.c4;
+  return o;
+}
+
 // VJP of (c1, c2, c3, c4) w.r.t. (Q, n, q_spatial, p_spatial) at the point described by g.
 template <typename R, bool Fast = false>
 __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, const Consts<R>& c,

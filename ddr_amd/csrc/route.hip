@@ -53,21 +53,49 @@ __device__ __forceinline__ unsigned long long load_granule(const double* p) {
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Spin until the granule is published (bounded).  On a timeout (or with the debug flag that forces
-// one) record it in the status block and return NaN: the corruption then shows in the outputs.
-__device__ double wait_granule(const double* p, unsigned* status, int bid, bool force_timeout) {
-  unsigned long long v = load_granule(p);
+// Spin until the granules of a chunk are published (bounded).  On a timeout (or with the debug flag
+// that forces one) record it in the status block and return NaN: the corruption then shows in the
+// outputs.
+// Granules requested together by one import batch (register budget: 2 VGPRs each).
+constexpr int kImportBatch = 4;
+// Batched form for the chunk imports: the granules row[t0 + s * stride] (s < C; outside [lo, hi):
+// 0) are all requested before the first wait, so a chunk costs one memory round trip, not C; only
+// the still-unpublished ones are polled again.
+template <int C>
+__device__ __forceinline__ void wait_granules(const double* row, int64_t t0, int stride, int64_t lo, int64_t hi,
+                                              double (&out)[C], unsigned* status, int bid, bool force_timeout) {
+  unsigned long long v[C];
+  unsigned pend = 0;
+#pragma unroll
+  for (int s = 0; s < C; ++s) {
+    const int64_t t = t0 + (int64_t)s * stride;
+    v[s] = (t >= lo && t < hi) ? load_granule(row + t) : 0ull;  // +0.0 outside the window
+  }
+#pragma unroll
+  for (int s = 0; s < C; ++s) pend |= (v[s] == kSentinel ? 1u : 0u) << s;
   unsigned spins = 0;
-  while (v == kSentinel || force_timeout) {
+  while (pend != 0u || force_timeout) {
     if (force_timeout || ++spins > (1u << 24)) {
       atomicAdd(status, 1u);
       atomicCAS(status + 1, 0u, (unsigned)bid + 1u);
-      return __builtin_nan("");
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int64_t t = t0 + (int64_t)s * stride;
+        const bool nan = ((pend >> s) & 1u) || (force_timeout && t >= lo && t < hi);
+        v[s] = nan ? 0x7FF8000000000000ull : v[s];
+      }
+      break;
     }
     __builtin_amdgcn_s_sleep(2);
-    v = load_granule(p);
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const unsigned long long w = ((pend >> s) & 1u) ? load_granule(row + (t0 + (int64_t)s * stride)) : v[s];
+      v[s] = w;
+      pend &= ~((w != kSentinel ? 1u : 0u) << s);
+    }
   }
-  return __longlong_as_double(v);
+#pragma unroll
+  for (int s = 0; s < C; ++s) out[s] = __longlong_as_double(v[s]);
 }
 
 // Logical block of this workgroup: the next ticket of the launch (forward: blocks in piece-height
@@ -85,6 +113,8 @@ __device__ __forceinline__ BlockDesc block_desc(const BlockDesc* blocks, int bid
   u.cout0 = __builtin_amdgcn_readfirstlane(d.cout0);
   u.ncout = __builtin_amdgcn_readfirstlane(d.ncout);
   u.dmax = __builtin_amdgcn_readfirstlane(d.dmax);
+  u.nxl = __builtin_amdgcn_readfirstlane(d.nxl);
+  u.xl0 = __builtin_amdgcn_readfirstlane(d.xl0);
   u.pad = 0;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(d.pre_dn & 0xffffffffu));
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)d.pre_dn >> 32));
@@ -109,18 +139,19 @@ __device__ __forceinline__ int take_ticket(unsigned* status, int word, int nbloc
 constexpr unsigned kWaitVmcnt0 = 0x0F70;
 
 // Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
+// pin_pow: keep the fp64 constants of the correctly rounded pow in VGPRs (kernels that evaluate it).
 template <typename R>
-__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a);
+__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a, bool pin_pow = true);
 template <>
-__device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a) {
+__device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a, bool pin_pow) {
 #ifndef DDR_PIN_POWK
 #define DDR_PIN_POWK 1
 #endif
   return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7],
-                       DDR_PIN_POWK ? pow_consts_vgpr() : pow_consts(), a.ln_dlb};
+                       (DDR_PIN_POWK && pin_pow) ? pow_consts_vgpr() : pow_consts(), a.ln_dlb};
 }
 template <>
-__device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a) {
+__device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a, bool) {
   return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7], pow_consts(), a.ln_dlb};
 }
 
@@ -135,13 +166,20 @@ __device__ __forceinline__ ReachStatic<R> load_static(const RouteArgs& a, int re
   return make_static<R>(n[ref], q[ref], p[(int64_t)ref * a.p_stride], S[ref], L[ref], X[ref]);
 }
 
-// Packed upstream descriptor: u0 (13 bits) | u1 (13 bits) << 13 | min(nup, 15) << 26; a missing
-// upstream reads slot `none` (the forward's zero slot).
+// Packed upstream descriptor: u0 (13 bits) | f1 (13 bits) << 13 | min(nup, 15) << 26; a missing
+// upstream reads slot `none` (the forward's zero slot).  f1 is the second upstream's slot, or for a
+// confluence (nup > 2) the offset of its list [c, u1, ..., u_{c-1}] in the block's LDS copy of
+// xlist: every upstream index of a tick comes from registers or LDS, never from a global load (whose
+// wait would also drain the tick's prefetches, in-order vmcnt).
 __device__ __forceinline__ unsigned pack_up(const RouteArgs& a, int P, unsigned none = 0u) {
   const int b = a.s.upb[P], c = a.s.upc[P];
   const unsigned u0 = c > 0 ? (unsigned)a.s.uplist[b] : none;
-  const unsigned u1 = c > 1 ? (unsigned)a.s.uplist[b + 1] : none;
+  const unsigned u1 = c > 2 ? (unsigned)a.s.xoff[P] : (c > 1 ? (unsigned)a.s.uplist[b + 1] : none);
   return u0 | (u1 << 13) | ((unsigned)(c < 15 ? c : 15) << 26);
+}
+// Copy the block's confluence lists into LDS (all threads; the caller synchronises).
+__device__ __forceinline__ void load_xlist(const RouteArgs& a, const BlockDesc& B, int* xl) {
+  for (int i = threadIdx.x; i < B.nxl; i += blockDim.x) xl[i] = a.s.xlist[B.xl0 + i];
 }
 // Make a per-reach value opaque inside the tick loop so the compiler recomputes what it derives
 // from it (64-bit addresses, qe + 1, ...) each tick instead of hoisting and keeping it live: at
@@ -161,7 +199,9 @@ __device__ __forceinline__ void store4(double* p, double a, double b, double c, 
   reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
 }
 __device__ __forceinline__ int up_0(unsigned u) { return (int)(u & 8191u); }
-__device__ __forceinline__ int up_1(unsigned u) { return (int)((u >> 13) & 8191u); }
+__device__ __forceinline__ int up_f1(unsigned u) { return (int)((u >> 13) & 8191u); }
+// slot of the second upstream (a confluence's from its LDS list)
+__device__ __forceinline__ int up_1(unsigned u, const int* xl) { return up_n(u) > 2 ? xl[up_f1(u) + 1] : up_f1(u); }
 
 // Debug per-workgroup profile (ddr_set_block_profile): start, end, import wait, hardware id.
 // Layout per workgroup: kProfWords uint64 = start, end, wait, hwid, then a timestamp every 1024 ticks.
@@ -182,6 +222,35 @@ __device__ __forceinline__ void prof_end(unsigned long long* p, int bid, unsigne
   p[1] = __builtin_amdgcn_s_memrealtime();
   p[2] = wait;
 }
+
+// Debug phase profile (-DDDR_PHASE_PROF=1 builds only): every wave accumulates the s_memtime cycles of
+// each tick phase; at the end lane 0 writes them after the per-block words of the profile buffer:
+// prof[kProfWords * nblocks + (bid * 16 + wave) * kPhases + phase].
+#ifndef DDR_PHASE_PROF
+#define DDR_PHASE_PROF 0
+#endif
+struct PhaseProf {
+#if DDR_PHASE_PROF
+  static constexpr int kPhases = 8;
+  unsigned long long acc[kPhases] = {};
+  unsigned long long t0 = 0;
+  __device__ __forceinline__ void start() { t0 = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void mark(int ph) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    acc[ph] += t - t0;
+    t0 = t;
+  }
+  __device__ __forceinline__ void flush(unsigned long long* prof, int nblocks, int bid) {
+    if (!prof || (threadIdx.x & 63)) return;
+    unsigned long long* q = prof + (size_t)kProfWords * nblocks + ((size_t)bid * 16 + (threadIdx.x >> 6)) * kPhases;
+    for (int i = 0; i < kPhases; ++i) q[i] = acc[i];
+  }
+#else
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void mark(int) {}
+  __device__ __forceinline__ void flush(unsigned long long*, int, int) {}
+#endif
+};
 
 }  // namespace
 
@@ -239,13 +308,22 @@ struct StatTab {
 #ifndef DDR_FWD_UNROLL2
 #define DDR_FWD_UNROLL2 1
 #endif
-template <typename R, int KR>
+// FM (fp32 only, DDR_FWD_FAST_MATH): the coefficients in hardware-approximate fp32 math
+// (coefficients_fast, the operation set of the adjoint's recompute) instead of the reference's exact
+// operation sequence; ~1e-6 relative per coefficient, and few enough registers that all of a
+// thread's slices run their physics in lockstep.
+template <typename R, int KR, bool FM>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
 #ifndef DDR_FWD_NP
 #define DDR_FWD_NP 1
 #endif
-  constexpr int NP = KR < DDR_FWD_NP ? KR : DDR_FWD_NP;  // slices whose physics runs in lockstep
+#ifndef DDR_FWD_NP_FAST
+#define DDR_FWD_NP_FAST 1
+#endif
+  constexpr bool kFast = FM && std::is_same<R, float>::value;
+  constexpr int NPW = kFast ? DDR_FWD_NP_FAST : DDR_FWD_NP;
+  constexpr int NP = KR < NPW ? KR : NPW;  // slices whose physics runs in lockstep
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bid = take_ticket(a.status, kStatusTicketFwd, a.nblocks, false, reinterpret_cast<int*>(smem));
   const BlockDesc B = block_desc(a.s.blocks, bid);
@@ -257,7 +335,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
   const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
-  const Consts<R> cs = consts_of<R>(a);
+  int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
+  const Consts<R> cs = consts_of<R>(a, !kFast);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool accum = a.flags & DDR_FWD_ACCUMULATE;  // every step a hot start (daily accumulation)
@@ -267,9 +346,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const R* q0p = static_cast<const R*>(a.q0);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
 
+  // off: tick offset (low 16 bits) | 1 + rank among the block's cut reaches (high 16, 0 = not cut;
+  // its boundary granule row is B.cout0 + rank, graph.cpp numbers cut edges that way)
   int ref[KR], off[KR];
   unsigned up[KR];
-  bool cut[KR];
+  auto off_of = [&](int k) { return off[k] & 0xFFFF; };
   R Q[KR], In[KR], qa[KR], qb[KR], ex[KR], inv[KR];  // ex, inv: the static divisions, kept in registers
   // runoff (N, T) written from here: the last four steps of each reach, stored 16 B at a time
   R ob0[KR], ob1[KR], ob2[KR], ob3[KR];
@@ -283,9 +364,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
-    off[k] = a.s.off[P];
+    const int e = a.s.cut[P];
+    off[k] = a.s.off[P] | (e >= 0 ? (e - B.cout0 + 1) << 16 : 0);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
-    cut[k] = a.s.cut[P] >= 0;
     Q[k] = In[k] = R(0);
     qa[k] = qb[k] = R(0);
     ob0[k] = ob1[k] = ob2[k] = ob3[k] = R(0);
@@ -296,12 +377,18 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   if (tid == 0) sx[S - 1] = 0.0;
   const bool vown = tid < B.nvirt;
-  int v_off = 0;
-  if (vown) v_off = a.s.v_off[B.virt0 + tid];
+  int v_off = 0, v_edge = 0;
+  if (vown) {
+    v_off = a.s.v_off[B.virt0 + tid];
+    v_edge = a.s.v_edge[B.virt0 + tid];
+  }
   load_math_tables();
+  load_xlist(a, B, xl);
   __syncthreads();
   unsigned long long prof_wait = 0;
   if (a.prof && tid == 0) prof_begin(a.prof, bid);
+  PhaseProf phz;
+  phz.start();
 
   // q'[max(t-1,0)] * flow_scale (gathered into the schedule layout: one row per tick), or the
   // carried Q0 at t = 0, for the step each reach runs at tick `tau`
@@ -312,7 +399,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k) {
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq0 + k * BS;
-      dst[k] = (carry && tau == off[k]) ? q0p[ref[k]] : row[r < B.nloc ? r : 0];
+      dst[k] = (carry && tau == off_of(k)) ? q0p[ref[k]] : row[r < B.nloc ? r : 0];
     }
   };
 
@@ -321,6 +408,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
+    phz.mark(0);  // the previous tick's loads and stores
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
     const int tq = opq(tid);
@@ -333,19 +421,23 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       inv[k] = opq(inv[k]);
     }
     if (B.nvirt > 0 && (tau % kChunk) == 0) {
-      // import the next chunk of every virtual inflow (x of the upstream block's reach)
+      // import the next chunk of every virtual inflow (x of the upstream block's reach): its owner
+      // thread requests the kChunk granules at once
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-      for (int w = tid; w < B.nvirt * kChunk; w += BS) {
-        const int v = w / kChunk, sidx = w % kChunk;
-        const int e = a.s.v_edge[B.virt0 + v];
-        const int t = tau + sidx - a.s.v_off[B.virt0 + v];
-        double val = 0.0;
-        if (t >= 0 && t < T) val = wait_granule(a.bnd + (int64_t)e * T + t, a.status, blockIdx.x, force_to);
-        ring[v * kChunk + sidx] = val;
+      if (vown) {
+#pragma unroll
+        for (int h = 0; h < kChunk; h += kImportBatch) {
+          double g[kImportBatch];
+          wait_granules<kImportBatch>(a.bnd + (int64_t)v_edge * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status, bid,
+                                      force_to);
+#pragma unroll
+          for (int i = 0; i < kImportBatch; ++i) ring[tid * kChunk + h + i] = g[i];
+        }
       }
       lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
+    phz.mark(1);  // import
     prefetch(tau + 1, qnext, tq);
     R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
@@ -365,7 +457,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         Qv[h] = Q[k0 + h];
       }
       if (!accum) {
-        coefficients_np<R, NP>(st, Qv, cs, ph);
+        if constexpr (kFast) {
+#pragma unroll
+          for (int h = 0; h < NP; ++h) ph[h] = coefficients_fast(st[h], Qv[h], cs);
+        } else {
+          coefficients_np<R, NP>(st, Qv, cs, ph);
+        }
       } else {
 #pragma unroll
         for (int h = 0; h < NP; ++h) ph[h] = PhysOut<R>{R(0), R(0), R(0), R(0), R(0), R(0)};
@@ -375,13 +472,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int k = k0 + h;
         const int r = tq + k * BS;
         const bool hk = r < B.nloc;
-        const int t = tau - off[k];
+        const int t = tau - off_of(k);
         const int nup = up_n(up[k]);
         const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
         const R qc = rmax(qv, cs.qlb);                                        // mmc.py:421-424
         const R b = ((ph[h].c2 * In[k]) + (ph[h].c3 * Q[k])) + (ph[h].c4 * qc);  // mmc.py:535-538
         const double x0v = sx[up_0(up[k])];
-        const double x1v = sx[up_1(up[k])];
+        const double x1v = sx[up_1(up[k], xl)];
         // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
         const bool raw = (t == 0 && carry);
         auto qf = [&](double x) -> R {
@@ -399,10 +496,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         inn = inn + (nup > 0 ? qf(x0v) : R(0));
         inn = inn + (nup > 1 ? qf(x1v) : R(0));
         if (nup > 2) {
-          const int P = B.pos0 + r;
-          const int bb = a.s.upb[P], c = a.s.upc[P];
+          const int* lst = xl + up_f1(up[k]);
+          const int c = lst[0];
           for (int j = 2; j < c; ++j) {
-            const double xj = sx[a.s.uplist[bb + j]];
+            const double xj = sx[lst[j]];
             acc = acc + dc1 * xj;
             hot = hot + xj;
             inn = inn + qf(xj);
@@ -424,7 +521,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
-          if (cut[k]) store_granule(a.bnd + (int64_t)a.s.cut[B.pos0 + r] * T + t, x);
+          if (off[k] >> 16) store_granule(a.bnd + (int64_t)(B.cout0 + (off[k] >> 16) - 1) * T + t, x);
           if (t == T - 1) {
             if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
             if (t > 0 && !accum) {
@@ -438,12 +535,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    phz.mark(2);  // prefetch issue + compute
     lds_barrier();
+    phz.mark(3);  // barrier 1
     // ---- publish ------------------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       if (wbase + k * BS >= B.nloc) continue;
-      const int t = tau - off[k];
+      const int t = tau - off_of(k);
       const int r = tq + k * BS;
       if (r < B.nloc && t >= 0 && t < T) sx[r] = xk[k];
     }
@@ -451,7 +550,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int t = tau - v_off;
       if (t >= 0 && t < T) sx[B.nloc + tid] = ring[tid * kChunk + (tau % kChunk)];
     }
+    phz.mark(4);  // publish
     lds_barrier();
+    phz.mark(5);  // barrier 2
   };
 
   const int TT = (int)T + B.dmax;
@@ -476,6 +577,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
 #endif
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
+  phz.flush(a.prof, a.nblocks, bid);
 }
 
 template <typename R>
@@ -518,6 +620,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   R* sx = sb + S;                                       // [S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
   const StatTab<R> tab{sx + S};                         // [S][6]
   R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * 9 * sizeof(R)));  // [ncout][kChunk][2]
+  int* xl = reinterpret_cast<int*>(smem + a.xl_off);                                            // confluence lists
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
@@ -528,11 +631,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
   const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
 
-  // od packs the tick offset (high 16 bits) and dl (low 16, signed): local downstream (>= 0),
-  // -(import slot + 2), or -1 -- one register for both
+  // od packs the tick offset (bits 16-30), dl (low 16, signed): local downstream (>= 0),
+  // -(import slot + 2), or -1, and bit 31: the reach has no dL/drunoff row (gauge mode, ungauged
+  // reach: its gradient loads, a dependent chain through the gauge map, are skipped)
   int ref[KR];
   unsigned od[KR];
-  auto off_of = [&](int k) { return (int)(od[k] >> 16); };
+  auto off_of = [&](int k) { return (int)((od[k] >> 16) & 0x7FFFu); };
+  auto has_grad = [&](int k) { return (od[k] >> 31) == 0u; };
   auto dl_of = [&](int k) { return (int)(short)(od[k] & 0xFFFFu); };
   unsigned up[KR];
   // xc = x(t), xa = x(t-1), xb = x(t-2) (published this tick, then reloaded with x(t-3), while
@@ -545,7 +650,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
-    od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu);
+    const bool nograd = a.g_roff != nullptr && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]];
+    od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu) | (nograd ? 0x80000000u : 0u);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
     lam[k] = sxn[k] = R(0);
     xc[k] = xa[k] = xb[k] = R(0);
@@ -561,17 +667,26 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   if (tid == 0) sx[S - 1] = R(0);
   const bool vown = tid < B.nvirt;
-  int v_edge = 0, v_off = 0, v_dloc = 0;
+  // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
+  // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
+  // tid < ncout: its import owner)
+  int v_edge = 0, v_off = 0;
+  unsigned* own = reinterpret_cast<unsigned*>(smem + a.own_off);
   if (vown) {
     v_edge = a.s.v_edge[B.virt0 + tid];
     v_off = a.s.v_off[B.virt0 + tid];
-    v_dloc = a.s.v_dloc[B.virt0 + tid];
   }
+  if (tid < B.nvirt || tid < B.ncout)
+    own[tid] = (vown ? (unsigned)a.s.v_dloc[B.virt0 + tid] & 0xFFFFu : 0u) |
+               (tid < B.ncout ? (unsigned)a.s.off[B.pos0 + a.s.cout_loc[B.cout0 + tid]] << 16 : 0u);
+  auto v_dloc_of = [&]() { return (int)(own[tid] & 0xFFFFu); };
   const int TT = (int)T + B.dmax;
   load_math_tables();
+  load_xlist(a, B, xl);
   __syncthreads();
   unsigned long long prof_wait = 0;
   if (a.prof && tid == 0) prof_begin(a.prof, bid);
+  PhaseProf phz;
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
   auto load_own = [&](int tau, R(&dst)[KR], int tq) {
@@ -640,6 +755,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // conservative count across the divergent load branches waits (vmcnt(0)) at the first use of a
     // previous-tick register, i.e. for the loads issued in THIS tick too.
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    phz.mark(0);  // the previous tick's loads and stores
     const int tq = opq(tid);
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -648,16 +764,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       up[k] = opq(up[k]);
     }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
+      // one (cut-out, step) per thread and iteration, its (A, B) granule pair requested together; the
+      // cut edge of cut-out c is B.cout0 + c (graph.cpp numbers cut edges in block order), its tick
+      // offset is in the owner words
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
       for (int w = tid; w < B.ncout * kChunk; w += BS) {
         const int c = w / kChunk, sidx = w % kChunk;
-        const int P = B.pos0 + a.s.cout_loc[B.cout0 + c];
-        const int e = a.s.cut[P];
-        const int t = (tau - sidx) - a.s.off[P];
+        const int t = (tau - sidx) - (int)(own[c] >> 16);
         R A = R(0), Bv = R(0);
         if (t >= 1 && t < T) {
-          A = R(wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2, a.status, bid, force_to));
-          Bv = R(wait_granule(a.bwd_bnd + ((int64_t)e * T + t) * 2 + 1, a.status, bid, force_to));
+          double g[2];
+          wait_granules<2>(a.bwd_bnd + ((int64_t)(B.cout0 + c) * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
+          A = R(g[0]);
+          Bv = R(g[1]);
         }
         ring[(c * kChunk + sidx) * 2] = A;
         ring[(c * kChunk + sidx) * 2 + 1] = Bv;
@@ -665,6 +784,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
+    phz.mark(1);  // import
     // ---- read / publish ----------------------------------------------------------------------
     if (vown) {
       // export the consumer's (c1 gb, c2 gb) of step t (written last tick, when the consumer ran
@@ -672,8 +792,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // at the consumer's current step - 1
       const int t = tau - v_off;
       if (t >= 1 && t < T) {
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[v_dloc]);
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[v_dloc]);
+        const int dloc = v_dloc_of();
+        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
+        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
       }
       sx[B.nloc + tid] = R(vx);
     }
@@ -695,7 +816,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         Bd[k] = ring[((-dl - 2) * kChunk + sidx) * 2 + 1];
       }
     }
+    phz.mark(2);  // read / publish
     lds_barrier();
+    phz.mark(3);  // barrier 1
     load_own(tau - 3, xb, tq);                    // x(t - 3), published next tick
     if (vown) vx = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
     // ---- compute ------------------------------------------------------------------------------
@@ -712,17 +835,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const bool c0 = (t == 1 && carry);
       const int nup = up_n(up[k]);
       const R x0 = sx[up_0(up[k])];
-      const R x1 = sx[up_1(up[k])];
+      const R x1 = sx[up_1(up[k], xl)];
       R sxv = R(0) + x0;
       sxv = sxv + x1;
       R I = R(0);
       I = I + (nup > 0 ? (c0 ? x0 : rmax(x0, cs.qlb)) : R(0));
       I = I + (nup > 1 ? (c0 ? x1 : rmax(x1, cs.qlb)) : R(0));
       if (nup > 2) {
-        const int P = B.pos0 + r;
-        const int bb = a.s.upb[P], c = a.s.upc[P];
+        const int* lst = xl + up_f1(up[k]);
+        const int c = lst[0];
         for (int j = 2; j < c; ++j) {
-          const R xj = sx[a.s.uplist[bb + j]];
+          const R xj = sx[lst[j]];
           sxv = sxv + xj;
           I = I + (c0 ? xj : rmax(xj, cs.qlb));
         }
@@ -771,13 +894,15 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
-      if (hk && tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)) {
+      if (hk && has_grad(k) && tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)) {
         const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3));
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    phz.mark(4);  // loads issue + compute
     lds_barrier();
+    phz.mark(5);  // barrier 2
     // next tick: x(t - 1) -> x(t); x(t - 2), still in the own slot -> x(t - 1)
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -804,11 +929,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const int r = tid + k * BS;
     if (r >= B.nloc) continue;
     R v = R(0) + sx[up_0(up[k])];
-    v = v + sx[up_1(up[k])];
+    v = v + sx[up_1(up[k], xl)];
     if (up_n(up[k]) > 2) {
-      const int P = B.pos0 + r;
-      const int bb = a.s.upb[P], c = a.s.upc[P];
-      for (int j = 2; j < c; ++j) v = v + sx[a.s.uplist[bb + j]];
+      const int* lst = xl + up_f1(up[k]);
+      for (int j = 2; j < lst[0]; ++j) v = v + sx[lst[j]];
     }
     sxn[k] = v;
   }
@@ -816,16 +940,18 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if (vown) vx = load_virt((int64_t)(TT - 1) - v_off - 2);
 #pragma unroll
   for (int k = 0; k < KR; ++k)
-    if (tid + k * BS < B.nloc && TT - 1 - off_of(k) == T - 1) {
+    if (tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
       const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3));
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
+  phz.start();
 #pragma unroll 1
   for (int tb = 0; tb < TT; ++tb) {
     if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
     tick(tb);
   }
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
+  phz.flush(a.prof, a.nblocks, bid);
 }
 
 // Final fp64 accumulators -> R gradients (reference order).
@@ -985,7 +1111,8 @@ __global__ void gauge_daily_seed_kernel(int64_t G, int64_t T, int64_t t0, int64_
 // ============================================================================================
 template <typename R>
 size_t route_smem_bytes(const Graph* g, bool backward) {
-  return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)(backward ? g->max_cout : g->max_virt), backward, sizeof(R));
+  return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt, (size_t)g->max_cout,
+                         (size_t)g->max_xl, backward, sizeof(R));
 }
 
 template <typename R, int KR>
@@ -994,6 +1121,8 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   a.slot_stride = route_slot_stride(g->max_slots);
   a.n_cut = g->n_cut;
   a.nblocks = (int32_t)g->blocks.size();
+  a.xl_off = (int32_t)(smem - (size_t)g->max_xl * 4);  // the lists close the LDS layout
+  a.own_off = a.xl_off - (int32_t)align16(4 * (size_t)std::max(g->max_virt, g->max_cout));
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
     auto kern = route_backward_kernel<R, KR>;
@@ -1006,7 +1135,9 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
     hipLaunchKernelGGL(finish_grads_kernel<R>, dim3(fb), dim3(256), 0, stream, g->n,
                        (const double*)(a.bwd_bnd + 2 * g->n_cut * a.T), (R*)a.gn, (R*)a.gq, (R*)a.gp);
   } else {
-    auto kern = route_forward_kernel<R, KR>;
+    auto kern = route_forward_kernel<R, KR, false>;
+    if constexpr (std::is_same<R, float>::value)
+      if (a.flags & DDR_FWD_FAST_MATH) kern = route_forward_kernel<R, KR, true>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
@@ -1029,9 +1160,9 @@ int max_resident_blocks(const Graph* g, bool backward) {
   const size_t smem = route_smem_bytes<R>(g, backward);
   const void* f = nullptr;
   switch (g->kr) {
-    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1>; break;
-    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2>; break;
-    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4>;
+    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1, false>; break;
+    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2, false>; break;
+    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4, false>;
   }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;

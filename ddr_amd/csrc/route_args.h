@@ -12,6 +12,8 @@ struct RouteArgs {
   int32_t flags;
   int32_t slot_stride;  // LDS slots per buffer (max nloc + nvirt over blocks)
   int32_t nblocks;      // logical blocks (tickets) of a routing launch
+  int32_t xl_off;       // byte offset of the confluence lists in the dynamic LDS
+  int32_t own_off;      // backward: byte offset of the hand-off owner words
   int32_t p_stride;
   int32_t qp_hours;               // hourly steps per stored q' row (1, or 24 for a daily store)
   int32_t qp_shift;               // step t reads q' row max(t - qp_shift, 0): 1 routing, 0 accumulation

@@ -341,8 +341,15 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
           length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor, *, flow_scale: torch.Tensor | None = None,
           q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
           save: bool | None = None, steps: int | None = None, qprime_hours: int = 1,
-          qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False):
+          qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False,
+          fast_math: bool = False):
     """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last).
+
+    ``fast_math`` (fp32): the forward's Muskingum coefficients in hardware-approximate fp32 math
+    (v_rcp / v_log / v_exp, the adjoint's operation set) instead of the reference's exact operation
+    sequence: ~1e-6 relative per coefficient, discharge within the stated 1e-4 of the reference
+    (tests/test_gpu_fastmath.py), no longer bit-identical to the oracle.  The backward is the same
+    either way.
 
     ``qprime_hours`` = 24 with ``steps`` = T routes a daily store (ceil(T / 24), N) indexed in-kernel
     (readers.py:513-519); ``qprime_valid`` (N, bool) marks divides present in the store, the others get
@@ -361,7 +368,7 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
     if save is None:
         save = (not accumulate) and torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
     flags = ((_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
-             | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0))
+             | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0) | (_lib.DDR_FWD_FAST_MATH if fast_math else 0))
     valid = None if qprime_valid is None else qprime_valid.to(device=dev, dtype=torch.uint8).contiguous()
     gid = register_graph(graph)
     gz = gauges

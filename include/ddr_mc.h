@@ -143,7 +143,7 @@ typedef struct {
  * DDR_FWD_ACCUMULATE: every step is a hot start, Q_t = max((I - N)^-1 q'_t, q_lb) with step t
  * reading q' row t -- the per-day discharge accumulation of scripts/geometry_predictor.py:193-212
  * (compute_hotstart_discharge, mmc.py:25-66) for all days in one launch. */
-enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8 };
+enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8, DDR_FWD_FAST_MATH = 16 };
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
  * Returns DDR_ERR_TIMEOUT instead of launching when an earlier launch's hand-off timed out
