@@ -176,6 +176,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dropin-steps", type=int, default=2, help="C5, 1 GPU: also time the drop-in dmc() path")
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
+    ap.add_argument("--stream", type=int, default=0,
+                    help="C3, 1 GPU: also time K training steps over K different batches (a new gauge-union "
+                         "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
+    ap.add_argument("--stream-workers", type=int, default=4)
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(fast_math=True))")
     args = ap.parse_args()
@@ -375,9 +379,78 @@ def main():
         }
         if dropin is not None:
             out["dropin_dmc"] = dropin
+        if args.workload == "c3" and world == 1 and args.stream > 0:
+            out["training_stream"] = time_training_stream(args, dev)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def time_training_stream(args, dev):
+    """C3 as a training loop sees it: every step a new batch of 256 gauged subnetworks, i.e. a new
+    adjacency, graph and gauge map per step (merit.py:197-223, scripts/train.py:54-104).  The graph of
+    every step is built anew on host threads (GraphPrefetcher, ``--stream-workers``) while the device
+    trains on the previous batch.  M = 4 distinct batches (inputs resident in HBM, generated before the
+    timed loop) are cycled over K steps; each step's timed region is the wait for its graph + upload +
+    the training step.  The first two steps are warm-up."""
+    from ddr_amd.distributed import allreduce_gradients
+    from ddr_amd.graph import GraphPrefetcher
+
+    K, T, M = args.stream, args.T, 4
+    t_gen = time.perf_counter()
+    data = []
+    window = DailyWindow.for_training(T, args.tau)
+    for k in range(M):
+        nt = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 100 + k), seed=100 + k, single_inflow=0.25)
+        at = synthetic.reach_attributes(nt.n, 200 + k)
+        tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        outlets = np.flatnonzero(nt.down < 0)
+        data.append(dict(net=nt, length=tt(at.length), slope=tt(np.maximum(at.slope, np.float32(1e-3))), xs=tt(at.x),
+                         feats=tt(synthetic.reach_features(nt.n, seed=200 + k)),
+                         qprime=synthetic.lateral_inflow_torch(nt.n, T, seed=200 + k, device=dev),
+                         gz=GaugeMap.build([np.array([o]) for o in outlets], nt.n, dev),
+                         obs=torch.from_numpy(np.random.default_rng(300 + k).lognormal(np.log(5.0), 1.0,
+                                              (len(outlets), window.D)).astype(np.float32)).to(dev)))
+    log(f"[stream] {M} batches resident in {time.perf_counter() - t_gen:.1f}s "
+        f"({min(d['net'].n for d in data)}..{max(d['net'].n for d in data)} reaches)")
+    model = ParamNet().to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    wd = args.warmup_days
+    consts = RouteConsts()
+    torch.cuda.synchronize()
+    warm = 2
+    pf = GraphPrefetcher(((data[k % M]["net"].n, data[k % M]["net"].rows, data[k % M]["net"].cols, k % M)
+                          for k in range(K + warm)), workers=args.stream_workers, steps_hint=T)
+    per = []
+    t_start = None
+    for k in range(K + warm):
+        if k == warm:
+            torch.cuda.synchronize()
+            t_start = time.perf_counter()
+        t0 = time.perf_counter()
+        g, m = next(pf)
+        t_graph = time.perf_counter() - t0
+        d = data[m]
+        opt.zero_grad(set_to_none=True)
+        un = model(d["feats"])
+        n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
+        daily, _, _, _ = route(g, d["qprime"], n, q, p, d["length"], d["slope"], d["xs"], gauges=d["gz"],
+                               daily=window, consts=consts)
+        loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])
+        loss.backward()
+        allreduce_gradients(list(model.parameters()))
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        opt.step()
+        if k >= warm:
+            per.append({"reaches": int(d["net"].n), "generations": g.info.generations, "blocks": g.info.n_blocks,
+                        "graph_wait_ms": round(t_graph * 1e3, 2)})
+    torch.cuda.synchronize()
+    timed = time.perf_counter() - t_start
+    pf.close()
+    rs = sum(b["reaches"] for b in per) * (T - 1)
+    return {"steps": K, "ms_per_step": timed / K * 1e3, "value": rs / timed, "unit": "reach-timesteps/s",
+            "graph_workers": args.stream_workers, "batches": per,
+            "note": f"new adjacency + graph build per step (overlapped on host threads), {M} distinct batches cycled"}
 
 
 def time_dropin(args, net, at, u, qprime, W, dev):

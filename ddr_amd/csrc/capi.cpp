@@ -123,6 +123,7 @@ ddr_status check_common(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   if (r->p_stride != 0 && r->p_stride != 1) return fail(DDR_ERR_ARG, "p_stride must be 0 or 1");
   if (r->qprime_hours < 0 || r->qprime_hours > (int64_t(1) << 20)) return fail(DDR_ERR_ARG, "bad qprime_hours");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
   if (T * (g->n + 1) > (int64_t(1) << 62)) return fail(DDR_ERR_ARG, "T * N overflows");
   return DDR_OK;
 }
@@ -258,6 +259,7 @@ ddr_status gauge_args(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   if (!gh || !x_save || !gz || T < 1) return fail(DDR_ERR_ARG, "bad gauge arguments");
   if (gz->n_gauges > 0 && (!gz->offsets || !gz->index)) return fail(DDR_ERR_ARG, "null gauge arrays");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
   std::memset(&a, 0, sizeof(a));
   a.s = g->dev;
   a.T = T;
@@ -332,6 +334,13 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
     if (st) return st;
     *out = reinterpret_cast<ddr_graph*>(g);
     return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_upload(ddr_graph* g) {
+  DDR_GUARD({
+    if (!g) return fail(DDR_ERR_ARG, "null graph");
+    return upload_schedule(reinterpret_cast<Graph*>(g));
   })
 }
 

@@ -13,6 +13,7 @@
 // one tick ("as late as possible" wavefront).  Large basins are split into connected pieces whose
 // inter-piece edges become cut edges exchanged through global memory.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -46,6 +47,35 @@ struct Piece {
 
 }  // namespace
 
+ddr_status upload_schedule(Graph* g) {
+  if (g->uploaded) return DDR_OK;
+  HostSchedule& H = g->hs;
+  DevSchedule& D = g->dev;
+  ddr_status st;
+  if ((st = upload(g, &D.blocks, g->blocks))) return st;
+  if ((st = upload(g, &D.ref, H.ref))) return st;
+  if ((st = upload(g, &D.off, H.off))) return st;
+  if ((st = upload(g, &D.upb, H.upb))) return st;
+  if ((st = upload(g, &D.upc, H.upc))) return st;
+  if ((st = upload(g, &D.dloc, H.dloc))) return st;
+  if ((st = upload(g, &D.cut, H.cut))) return st;
+  if ((st = upload(g, &D.uplist, H.uplist))) return st;
+  if ((st = upload(g, &D.xoff, H.xoff))) return st;
+  if ((st = upload(g, &D.xlist, H.xlist))) return st;
+  if ((st = upload(g, &D.v_edge, H.v_edge))) return st;
+  if ((st = upload(g, &D.v_off, H.v_off))) return st;
+  if ((st = upload(g, &D.v_dloc, H.v_dloc))) return st;
+  if ((st = upload(g, &D.cout_loc, H.cout_loc))) return st;
+  if ((st = upload(g, &D.pos_of_ref, H.pos_of_ref))) return st;
+  if ((st = upload(g, &D.block_of_pos, H.block_of_pos))) return st;
+  if ((st = upload(g, &D.rs_loc, H.rs_loc))) return st;
+  if ((st = upload(g, &D.rs_ref, H.rs_ref))) return st;
+  DDR_HIP(hipGetDevice(&g->device));
+  g->uploaded = true;
+  g->hs = HostSchedule{};  // the device copy is the schedule from here on
+  return DDR_OK;
+}
+
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out) {
   if (n <= 0) return fail(DDR_ERR_ARG, "graph must have at least one reach");
@@ -53,6 +83,15 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   if (e < 0 || (e > 0 && (!rows || !cols))) return fail(DDR_ERR_ARG, "bad COO arrays");
   auto g = std::make_unique<Graph>();
   g->n = n;
+  const bool dbg = getenv("DDR_DEBUG_PART") != nullptr;
+  auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double tp = tnow();
+  auto phase = [&](const char* what) {
+    if (!dbg) return;
+    const double t = tnow();
+    fprintf(stderr, "[part] %-10s %8.2f ms\n", what, t - tp);
+    tp = t;
+  };
   // ---- validation + canonical CSR (counting sort by row, then ascending columns) ----------
   std::vector<int64_t> cnt(n + 1, 0);
   for (int64_t k = 0; k < e; ++k) {
@@ -66,13 +105,18 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   for (int64_t i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
   std::vector<int64_t> col(e), fill(cnt.begin(), cnt.end() - 1);
   for (int64_t k = 0; k < e; ++k) col[fill[rows[k]]++] = cols[k];
-  for (int64_t i = 0; i < n; ++i) std::sort(col.begin() + cnt[i], col.begin() + cnt[i + 1]);
+  for (int64_t i = 0; i < n; ++i) {  // rows hold a few entries: insertion sort
+    for (int64_t k = cnt[i] + 1; k < cnt[i + 1]; ++k) {
+      const int64_t v = col[k];
+      int64_t j = k;
+      for (; j > cnt[i] && col[j - 1] > v; --j) col[j] = col[j - 1];
+      col[j] = v;
+    }
+  }
   for (int64_t i = 0; i < n; ++i)
     for (int64_t k = cnt[i] + 1; k < cnt[i + 1]; ++k)
       if (col[k] == col[k - 1])
         return fail(DDR_ERR_DUPLICATE, "duplicate edge (" + std::to_string(i) + "," + std::to_string(col[k]) + ")");
-  g->crow = cnt;
-  g->col = col;
   g->nnz = e;
   // ---- dendritic structure ---------------------------------------------------------------
   g->down.assign(n, -1);
@@ -91,9 +135,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     g->basin[i] = d < 0 ? i : g->basin[d];
   }
   g->max_depth = n ? *std::max_element(g->dist.begin(), g->dist.end()) + 1 : 0;
-  std::vector<int64_t> bsize(n, 0);
-  for (int64_t i = 0; i < n; ++i) bsize[g->basin[i]]++;
   for (int64_t i = 0; i < n; ++i) g->n_basins += (g->down[i] < 0);
+  phase("csr+tree");
 
   // ---- partition: split basins larger than cap into connected pieces ---------------------
   int dev = 0, n_cu = 0, resident = 0;
@@ -113,13 +156,13 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
 
   // Splitting works on full-subtree sizes and heights: sub(i) = reaches draining through i,
   // ht(i) = longest path from i up to a source.
-  std::vector<int64_t> sub(n, 1), ht(n, 0);
+  std::vector<int32_t> sub(n, 1), ht(n, 0);
   for (int64_t i = 0; i < n; ++i)
     for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
       sub[i] += sub[col[k]];
       ht[i] = std::max(ht[i], ht[col[k]] + 1);
     }
-  std::vector<int64_t> piece(n), resid(n), stem(n), dloc_piece(n);
+  std::vector<int32_t> piece(n), resid(n), stem(n), dloc_piece(n);
   std::vector<char> is_root(n);
   std::vector<Piece> pieces;
   std::vector<int64_t> others;
@@ -189,7 +232,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       Piece& P = pieces[piece[i]];
       P.size++;
       if (cnt[i + 1] - cnt[i] > 2) P.xl += cnt[i + 1] - cnt[i];
-      P.dmax = std::max(P.dmax, dloc_piece[i]);
+      P.dmax = std::max<int64_t>(P.dmax, dloc_piece[i]);
     }
     // virtual inflows deepen the consuming piece by one tick; piece heights (children first:
     // a child piece is created after its parent in the loop above)
@@ -197,10 +240,11 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       int64_t r = pieces[p].root, d = g->down[r];
       if (d >= 0) {
         Piece& Q = pieces[piece[d]];
-        Q.dmax = std::max(Q.dmax, dloc_piece[d] + 1);
+        Q.dmax = std::max<int64_t>(Q.dmax, dloc_piece[d] + 1);
         Q.height = std::max(Q.height, pieces[p].height + 1);
       }
     }
+    phase("split");
     int64_t ncut = 0;
     for (auto& P : pieces) ncut += (g->down[P.root] >= 0);
     // Packing: pieces of equal height share blocks (so the block dependency graph is a DAG),
@@ -237,7 +281,14 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     int64_t ncut0 = 0;
     for (auto& P : pieces) ncut0 += (g->down[P.root] >= 0);
     const int64_t limit = ncut0 > 0 ? std::min<int64_t>(target, resident) * gen : target;
-    for (double capw = wsum / (double)limit;; capw *= 1.01) {
+    // capw_k = capw_0 * 1.01^k; beyond k_sat (capw / fac >= hard_cap for every piece) the packing no
+    // longer changes.  The block count falls with k, so the smallest k that fits is binary-searched
+    // (a handful of packing passes instead of one per 1 % step).
+    double maxfac = 1.0;
+    for (double f : fac) maxfac = std::max(maxfac, f);
+    const double capw0 = wsum / (double)limit;
+    auto pack = [&](int k) {
+      const double capw = capw0 * std::pow(1.01, (double)k);
       load.clear();
       bcap.clear();
       size_t hstart = 0;  // first block of the current height class
@@ -248,19 +299,38 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
           hstart = load.size();
         }
         int64_t best = -1;
+        const int64_t sz = pieces[p].size;
         for (size_t b = hstart; b < load.size(); ++b)
-          if ((double)(load[b] + pieces[p].size) <= bcap[b] && (best < 0 || load[b] < load[best])) best = (int64_t)b;
+          if ((double)(load[b] + sz) <= bcap[b] && (best < 0 || load[b] < load[best])) best = (int64_t)b;
         if (best < 0) {
           best = (int64_t)load.size();
           load.push_back(0);
-          bcap.push_back(std::min<double>((double)hard_cap, std::max<double>((double)pieces[p].size, capw / fac[p])));
+          bcap.push_back(std::min<double>((double)hard_cap, std::max<double>((double)sz, capw / fac[p])));
         }
-        load[best] += pieces[p].size;
+        load[best] += sz;
         block_of_piece[p] = best;
       }
-      if ((int64_t)load.size() <= limit || capw / 1.3 > (double)hard_cap) break;
+      return (int64_t)load.size();
+    };
+    const int k_sat = std::max(0, (int)std::ceil(std::log((double)hard_cap * maxfac / capw0) / std::log(1.01)));
+    int npass = 1;
+    if (pack(0) > limit) {
+      int lo = 0, hi = k_sat;  // pack(lo) > limit; find the smallest k in (lo, hi] with pack(k) <= limit
+      ++npass;
+      if (pack(hi) <= limit) {
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) / 2;
+          ++npass;
+          if (pack(mid) <= limit) hi = mid;
+          else lo = mid;
+        }
+        ++npass;
+        pack(hi);
+      }
     }
     const int64_t nblocks = (int64_t)load.size();
+    if (dbg) fprintf(stderr, "[part] pack passes %d\n", npass);
+    phase("pack");
     if (getenv("DDR_DEBUG_PART"))
       fprintf(stderr, "[part] cap %ld hard %ld gen %ld weighted %d pieces %zu blocks %ld cut %ld\n", (long)cap,
               (long)hard_cap, (long)gen, (int)weighted, pieces.size(), (long)nblocks, (long)ncut);
@@ -287,7 +357,10 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
                                    route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
       if (getenv("DDR_DEBUG_PART"))
         fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
-      if (need > kLdsBudget || mx >= kMaxConfluenceList) {
+      // (a count failure at the capacity ceiling of the unweighted packing goes to more generations:
+      // shrinking the capacity for LDS would only add blocks)
+      const bool count_dead = ncut > 0 && nblocks > limit && cap >= hard_cap && !weighted;
+      if (!count_dead && (need > kLdsBudget || mx >= kMaxConfluenceList)) {
         if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
         hard_cap -= std::max<int64_t>(1, hard_cap / 32);
         cap = std::min(cap, hard_cap);
@@ -310,6 +383,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + per_gen - 1) / per_gen));
       continue;
     }
+    phase("lds");
     g->generations = gen;
     g->resident = resident;
     // ---- emit the schedule ---------------------------------------------------------------
@@ -317,39 +391,72 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     g->n_cut = ncut;
     g->block_of.assign(n, 0);
     for (int64_t i = 0; i < n; ++i) g->block_of[i] = block_of_piece[piece[i]];
-    std::vector<std::vector<int64_t>> members(nblocks);
-    for (int64_t i = 0; i < n; ++i) members[g->block_of[i]].push_back(i);
     std::vector<int64_t> bdmax(nblocks, 0);
     for (size_t p = 0; p < pieces.size(); ++p)
       bdmax[block_of_piece[p]] = std::max(bdmax[block_of_piece[p]], pieces[p].dmax);
-    std::vector<int64_t> offv(n);
+    std::vector<int32_t> offv(n);
     for (int64_t i = 0; i < n; ++i) offv[i] = bdmax[g->block_of[i]] - dloc_piece[i];
+    // internal order (block, tick offset, reference index): two stable counting sorts over the
+    // ascending reach ids, by offset and then by block (O(n), no comparison sort)
+    std::vector<int64_t> bstart(nblocks + 1, 0);
+    std::vector<int32_t> order_all(n);
+    {
+      int64_t omax = 0;
+      for (int64_t b = 0; b < nblocks; ++b) omax = std::max(omax, bdmax[b]);
+      std::vector<int64_t> oc(omax + 2, 0);
+      for (int64_t i = 0; i < n; ++i) oc[offv[i] + 1]++;
+      for (int64_t o = 0; o <= omax; ++o) oc[o + 1] += oc[o];
+      std::vector<int32_t> by_off(n);
+      for (int64_t i = 0; i < n; ++i) by_off[oc[offv[i]]++] = (int32_t)i;
+      for (int64_t i = 0; i < n; ++i) bstart[g->block_of[i] + 1]++;
+      for (int64_t b = 0; b < nblocks; ++b) bstart[b + 1] += bstart[b];
+      std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
+      for (int64_t j = 0; j < n; ++j) {
+        const int32_t i = by_off[j];
+        order_all[fillb[g->block_of[i]]++] = i;
+      }
+    }
+    struct Span {
+      const int32_t* b;
+      const int32_t* e;
+      const int32_t* begin() const { return b; }
+      const int32_t* end() const { return e; }
+      size_t size() const { return (size_t)(e - b); }
+      int64_t operator[](size_t k) const { return b[k]; }
+    };
+    auto members_of = [&](int64_t b) { return Span{order_all.data() + bstart[b], order_all.data() + bstart[b + 1]}; };
+    phase("members");
     // internal order: blocks contiguous; inside a block by (tick offset, reference index)
-    std::vector<int64_t> pos(n), local(n);
-    std::vector<int32_t> ref(n), offs(n), upb(n), upc(n), dl(n), cut(n, -1), xoff(n, -1), uplist;
-    std::vector<int32_t> v_edge, v_off, v_dloc, cout_loc;
-    std::vector<int64_t> edge_id(n, -1);
+    std::vector<int32_t> pos(n), local(n);
+    HostSchedule& H = g->hs;
+    H = HostSchedule{};
+    std::vector<int32_t>&ref = H.ref, &offs = H.off, &upb = H.upb, &upc = H.upc, &dl = H.dloc, &cut = H.cut,
+                        &xoff = H.xoff, &uplist = H.uplist, &xlist = H.xlist, &v_edge = H.v_edge, &v_off = H.v_off,
+                        &v_dloc = H.v_dloc, &cout_loc = H.cout_loc;
+    ref.resize(n);
+    offs.resize(n);
+    upb.resize(n);
+    upc.resize(n);
+    dl.resize(n);
+    cut.assign(n, -1);
+    xoff.assign(n, -1);
+    std::vector<int32_t> edge_id(n, -1);
     // Cut edges are numbered in (block, local position) order, i.e. by their index in cout_loc: the
     // forward kernel derives a cut reach's granule row from B.cout0 + its rank among the block's
     // cut reaches (route.hip), with no table load in the tick.
-    for (int64_t b = 0; b < nblocks; ++b)
-      std::stable_sort(members[b].begin(), members[b].end(), [&](int64_t a, int64_t c) {
-        if (offv[a] != offv[c]) return offv[a] < offv[c];
-        return a < c;
-      });
+    phase("sort");
     int64_t eid = 0;
     for (int64_t b = 0; b < nblocks; ++b)
-      for (int64_t i : members[b])
+      for (int64_t i : members_of(b))
         if (g->down[i] >= 0 && g->block_of[g->down[i]] != b) edge_id[i] = eid++;
     g->n_cut = eid;  // inter-workgroup edges (pieces packed into one block hand off in LDS)
-    std::vector<int32_t> xlist;
     g->blocks.assign(nblocks, BlockDesc{});
     int64_t p0 = 0, pre_dn = 0;
     g->max_slots = g->max_virt = g->max_cout = g->max_xl = 0;
     g->max_block_depth = 0;
     int64_t max_load = 0;
     for (int64_t b = 0; b < nblocks; ++b) {
-      auto& m = members[b];
+      const Span m = members_of(b);
       for (size_t r = 0; r < m.size(); ++r) {
         pos[m[r]] = p0 + (int64_t)r;
         local[m[r]] = (int64_t)r;
@@ -406,6 +513,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       pre_dn += bdmax[b] * (int64_t)m.size();
       p0 += (int64_t)m.size();
     }
+    phase("emit");
     for (int64_t i = 0; i < n; ++i) {
       int64_t P = pos[i];
       if (dl[P] == -2) dl[P] = (int32_t)local[g->down[i]];
@@ -417,47 +525,41 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     g->kr = kr;
     if (g->max_virt > bs || g->max_cout > bs)
       return fail(DDR_ERR_CAPACITY, "too many inter-workgroup edges in one workgroup");
-    // ---- upload ----------------------------------------------------------------------------
-    if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) break;
-    DevSchedule& D = g->dev;
-    ddr_status st;
-    if ((st = upload(g.get(), &D.blocks, g->blocks))) return st;
-    if ((st = upload(g.get(), &D.ref, ref))) return st;
-    if ((st = upload(g.get(), &D.off, offs))) return st;
-    if ((st = upload(g.get(), &D.upb, upb))) return st;
-    if ((st = upload(g.get(), &D.upc, upc))) return st;
-    if ((st = upload(g.get(), &D.dloc, dl))) return st;
-    if ((st = upload(g.get(), &D.cut, cut))) return st;
-    if ((st = upload(g.get(), &D.uplist, uplist))) return st;
-    if ((st = upload(g.get(), &D.xoff, xoff))) return st;
-    if ((st = upload(g.get(), &D.xlist, xlist))) return st;
-    if ((st = upload(g.get(), &D.v_edge, v_edge))) return st;
-    if ((st = upload(g.get(), &D.v_off, v_off))) return st;
-    if ((st = upload(g.get(), &D.v_dloc, v_dloc))) return st;
-    if ((st = upload(g.get(), &D.cout_loc, cout_loc))) return st;
-    std::vector<int32_t> pos_of_ref(n), block_of_pos(n);
-    for (int64_t i = 0; i < n; ++i) {
-      pos_of_ref[i] = (int32_t)pos[i];
-      block_of_pos[pos[i]] = (int32_t)g->block_of[i];
+    phase("schedule");
+    if (dbg) {  // schedule fingerprint (FNV-1a over the emitted arrays)
+      unsigned long long h = 1469598103934665603ull;
+      auto mix = [&](const std::vector<int32_t>& v) {
+        for (int32_t x : v) h = (h ^ (unsigned)x) * 1099511628211ull;
+      };
+      mix(ref); mix(offs); mix(upb); mix(upc); mix(dl); mix(cut); mix(xoff); mix(uplist); mix(xlist);
+      mix(v_edge); mix(v_off); mix(v_dloc); mix(cout_loc);
+      fprintf(stderr, "[part] schedule fingerprint %016llx\n", h);
     }
-    if ((st = upload(g.get(), &D.pos_of_ref, pos_of_ref))) return st;
-    if ((st = upload(g.get(), &D.block_of_pos, block_of_pos))) return st;
-    // per block: local indices in ascending reference order (coalesced reads of q' rows)
-    std::vector<int32_t> rs_loc(n), rs_ref(n);
-    for (int64_t b = 0; b < nblocks; ++b) {
-      const BlockDesc& B = g->blocks[b];
-      std::vector<std::pair<int32_t, int32_t>> v(B.nloc);
-      for (int32_t r = 0; r < B.nloc; ++r) v[r] = {ref[B.pos0 + r], r};
-      std::sort(v.begin(), v.end());
-      for (int32_t k = 0; k < B.nloc; ++k) {
-        rs_ref[B.pos0 + k] = v[k].first;
-        rs_loc[B.pos0 + k] = v[k].second;
+    // reference-order views for the q' gather: pos_of_ref, block_of_pos, and per block its local
+    // indices in ascending reference order (a stable counting sort of the reach ids by block)
+    H.pos_of_ref.resize(n);
+    H.block_of_pos.resize(n);
+    H.rs_loc.resize(n);
+    H.rs_ref.resize(n);
+    {
+      std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
+      for (int64_t i = 0; i < n; ++i) {
+        H.pos_of_ref[i] = pos[i];
+        H.block_of_pos[pos[i]] = (int32_t)g->block_of[i];
+        const int64_t k = fillb[g->block_of[i]]++;
+        H.rs_ref[k] = (int32_t)i;
+        H.rs_loc[k] = local[i];
       }
     }
-    if ((st = upload(g.get(), &D.rs_loc, rs_loc))) return st;
-    if ((st = upload(g.get(), &D.rs_ref, rs_ref))) return st;
+    phase("views");
+    if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) break;
+    ddr_status st = upload_schedule(g.get());
+    if (st) return st;
+    phase("upload");
     break;
   }
+  g->crow = std::move(cnt);
+  g->col = std::move(col);
   *out = g.release();
   return DDR_OK;
 }

@@ -100,6 +100,12 @@ struct DevSchedule {
   int32_t* rs_ref = nullptr;       // (N) the matching reference indices
 };
 
+// The same schedule on the host (built by build_graph; released once uploaded).
+struct HostSchedule {
+  std::vector<int32_t> ref, off, upb, upc, dloc, cut, uplist, xoff, xlist, v_edge, v_off, v_dloc, cout_loc;
+  std::vector<int32_t> pos_of_ref, block_of_pos, rs_loc, rs_ref;
+};
+
 struct Graph {
   int64_t n = 0, nnz = 0;
   std::vector<int64_t> crow, col;
@@ -115,7 +121,9 @@ struct Graph {
   int max_nloc = 0;      // largest block
   int64_t generations = 1;  // ceil(blocks / resident) the packer aimed for (1: all blocks co-resident)
   int64_t resident = 0;     // co-resident workgroups assumed by the packer
+  HostSchedule hs;
   DevSchedule dev;
+  bool uploaded = false;
   std::vector<void*> allocations;
 };
 
@@ -135,6 +143,8 @@ const char* last_error_cstr();
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out);
 void destroy_graph(Graph* g);
+// Upload a host-built schedule (DDR_BUILD_HOST_ONLY) to the current device; no-op once uploaded.
+ddr_status upload_schedule(Graph* g);
 
 // Status block layout (device, zeroed before every launch): word 0 = timed-out hand-offs, word 1 =
 // first failing block + 1, word 2 = forward ticket counter, word 3 = backward ticket counter.

@@ -87,6 +87,11 @@ typedef struct {
  * Synchronous (the only host-synchronising call besides ddr_graph_status). */
 ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                            const ddr_build_opts* opts, ddr_graph** out);
+/* Upload the schedule of a graph built with DDR_BUILD_HOST_ONLY to the current HIP device (no-op
+ * if already uploaded).  The host build needs no device: it can run on any host thread (e.g. a
+ * data-loader worker preparing the next training batch, merit.py:197-223) while the device routes
+ * the current one; only this step touches the device.  Synchronous. */
+ddr_status ddr_graph_upload(ddr_graph* g);
 /* Any graph size builds: workgroups take ticket-ordered logical blocks, so a schedule with more
  * blocks than co-resident workgroups still completes (ddr_graph_info.generations > 1). */
 ddr_status ddr_graph_destroy(ddr_graph* g);

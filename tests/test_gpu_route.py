@@ -30,7 +30,8 @@ def consts_of(case):
                        bottom_width_lb=m["bottom_width"])
 
 
-def run_hip(case, dev, dtype=torch.float32, gkw=None, gauges=None, q0=None, qprime=None, W=None, grads=True):
+def run_hip(case, dev, dtype=torch.float32, gkw=None, gauges=None, q0=None, qprime=None, W=None, grads=True,
+            graph=None):
     """Reference recipe on the device: denormalize in torch, fused route, backward(W)."""
     rng = case.params["parameter_ranges"]
     ls = case.params["log_space_parameters"]
@@ -41,7 +42,7 @@ def run_hip(case, dev, dtype=torch.float32, gkw=None, gauges=None, q0=None, qpri
     p = (denormalize(u["p_spatial"], rng["p_spatial"], "p_spatial" in ls) if u.get("p_spatial") is not None
          else torch.tensor(float(case.params["defaults"]["p_spatial"]), device=dev, dtype=dtype))
     slope = torch.clamp(tt(case.slope), min=case.params["attribute_minimums"]["slope"])
-    g = RiverGraph(case.n, case.rows, case.cols, **(gkw or {}))
+    g = graph if graph is not None else RiverGraph(case.n, case.rows, case.cols, **(gkw or {}))
     qp = tt(case.qprime if qprime is None else qprime)
     runoff, q_last, tw, ss = route(g, qp, n, q, p, tt(case.length), slope, tt(case.x), gauges=gauges,
                                    q0=None if q0 is None else tt(q0), consts=consts_of(case))
@@ -283,3 +284,35 @@ def test_forced_timeout_raises_on_next_call(cuda):
     ok = run_hip(case, cuda, gkw=gkw)
     assert np.isfinite(ok["runoff"]).all()
     check_status()
+
+
+def test_prefetched_batches_match_oracle(cuda):
+    """Training-style use: every batch a new adjacency, built on worker threads (GraphPrefetcher) and
+    uploaded on the consumer's thread; each routes exactly as the oracle."""
+    from ddr_amd.graph import GraphPrefetcher
+
+    cases = [synthetic_case(synthetic.forest(synthetic.loguniform_sizes(6, 50, 800, s), seed=s), 40, s)
+             for s in range(3)]
+    pf = GraphPrefetcher(((c.n, c.rows, c.cols, c) for c in cases), workers=2, max_block_reaches=128,
+                         target_blocks=1 << 20)
+    seen = 0
+    for g, case in pf:
+        assert not g.host_only and g.info.n_cut > 0
+        res = run_hip(case, cuda, graph=g)
+        ref = O.route(case.network(), res["reaches"], case.qprime, case.bounds, dtype=np.float32)
+        assert maxrel(res["runoff"], ref["runoff"]) <= 1e-6
+        seen += 1
+    assert seen == 3
+
+
+def test_host_only_graph_is_refused_until_uploaded(cuda):
+    from ddr_amd import _lib
+
+    case = synthetic_case(synthetic.random_binary_tree(200, 5), 12, 5)
+    g = RiverGraph(case.n, case.rows, case.cols, host_only=True)
+    with pytest.raises(_lib.DDRError):
+        run_hip(case, cuda, graph=g, grads=False)
+    g.upload(cuda)
+    res = run_hip(case, cuda, graph=g, grads=False)
+    ref = O.route(case.network(), res["reaches"], case.qprime, case.bounds, dtype=np.float32)
+    assert maxrel(res["runoff"], ref["runoff"]) <= 1e-6

@@ -159,3 +159,31 @@ def test_adjacency_layouts_agree():
         assert n == ref[0]
         np.testing.assert_array_equal(r[order], ref[1])
         np.testing.assert_array_equal(c[order], ref[2])
+
+
+def test_prefetcher_builds_match_serial_builds():
+    """GraphPrefetcher's worker-thread builds are the same schedules as serial builds, in order."""
+    from ddr_amd.graph import GraphPrefetcher
+
+    nets = [synthetic.forest(synthetic.loguniform_sizes(12, 50, 2000, s), seed=s) for s in range(5)]
+    pf = GraphPrefetcher(((nt.n, nt.rows, nt.cols, k) for k, nt in enumerate(nets)), workers=3, depth=2,
+                         upload=False, max_block_reaches=256, target_blocks=16)
+    got = list(pf)
+    assert [k for _, k in got] == list(range(5))
+    for (g, k), nt in zip(got, nets):
+        ref = host_graph(nt.n, nt.rows, nt.cols, max_block_reaches=256, target_blocks=16)
+        assert g.info == ref.info
+        for key in ("down", "dist", "basin", "block"):
+            np.testing.assert_array_equal(g.structure()[key], ref.structure()[key])
+
+
+def test_generation_fallback_builds_fast():
+    """A batch just over the one-generation capacity goes straight to two generations (no futile
+    capacity shrinking), and the capacity search stays a handful of packing passes."""
+    import time
+
+    net = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 1), seed=1, single_inflow=0.25)
+    t = time.perf_counter()
+    g = host_graph(net.n, net.rows, net.cols, steps_hint=2136, max_resident=256, target_blocks=256)
+    assert time.perf_counter() - t < 5.0
+    assert g.info.generations == 2 and g.info.n_blocks <= 512
