@@ -337,6 +337,16 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
   })
 }
 
+ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
+                              const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
+                              int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
+                              int32_t* gage_c) {
+  DDR_GUARD({
+    return collate_gauges(n_conus, n_gauges, sub_off, rows, cols, gage_idx, active, n_active, crow, col, nnz,
+                          out_off, out_idx, gage_c);
+  })
+}
+
 ddr_status ddr_graph_upload(ddr_graph* g) {
   DDR_GUARD({
     if (!g) return fail(DDR_ERR_ARG, "null graph");

@@ -143,6 +143,11 @@ const char* last_error_cstr();
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out);
 void destroy_graph(Graph* g);
+// collate.cpp: per-batch gauge union (ddr_collate_gauges)
+ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
+                          const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
+                          int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
+                          int32_t* gage_c);
 // Upload a host-built schedule (DDR_BUILD_HOST_ONLY) to the current device; no-op once uploaded.
 ddr_status upload_schedule(Graph* g);
 

@@ -10,7 +10,10 @@
  * Reference interfaces each entry point replaces (file:line in /root/reference):
  *   ddr_graph_build     src/ddr/geodatazoo/merit.py:197-223 (COO union -> scipy .tocsr())
  *                       + src/ddr/routing/utils.py:25-163 (PatternMapper / get_network_idx)
+ *   ddr_graph_upload    (host build on a loader thread, then upload: the per-batch graph of training)
  *   ddr_graph_csr       scipy.sparse.coo_matrix(...).tocsr() canonical CSR (bit-exact target)
+ *   ddr_collate_gauges  src/ddr/io/builders.py:55-109 construct_network_matrix + merit.py:197-238
+ *                       (per-batch gauge union, compression, outflow_idx)
  *   ddr_mc_forward      src/ddr/routing/mmc.py:365-443 (MuskingumCunge.forward) with
  *                       mmc.py:487-559 (route_timestep), mmc.py:25-66 (compute_hotstart_discharge),
  *                       mmc.py:102-168 + geometry/trapezoidal.py:14-108 (celerity),
@@ -87,6 +90,22 @@ typedef struct {
  * Synchronous (the only host-synchronising call besides ddr_graph_status). */
 ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                            const ddr_build_opts* opts, ddr_graph** out);
+/* Per-batch gauge union, replacing construct_network_matrix (src/ddr/io/builders.py:55-109) and the
+ * compression steps of Merit._collate_gages (src/ddr/geodatazoo/merit.py:197-238; Lynker twin
+ * lynker_hydrofabric.py:198-266).  Host, O(E + n_conus), no device.
+ *   in : n_conus; n_gauges subsets as one COO in CONUS numbering, subset g = entries
+ *        [sub_off[g], sub_off[g+1]) of rows (downstream) / cols (upstream); gage_idx[g] (CONUS).
+ *   out: active[n_active] CONUS ids of the union's reaches, ascending (capacity: min(n_conus,
+ *        2 E + n_gauges)); crow[n_active + 1], col[nnz] canonical CSR of the compressed union
+ *        (capacity of col: E); out_off[n_gauges + 1], out_idx (capacity E + n_gauges): outflow_idx
+ *        of each gauge, the compressed upstream reaches of its reach ascending (itself when it has
+ *        none); gage_c[n_gauges] each gauge's compressed index.
+ * Rejects non-lower-triangular entries (DDR_ERR_NOT_LOWER) and a union in which a reach drains into
+ * two reaches (DDR_ERR_NOT_DENDRITIC). */
+ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
+                              const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
+                              int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
+                              int32_t* gage_c);
 /* Upload the schedule of a graph built with DDR_BUILD_HOST_ONLY to the current HIP device (no-op
  * if already uploaded).  The host build needs no device: it can run on any host thread (e.g. a
  * data-loader worker preparing the next training batch, merit.py:197-223) while the device routes

@@ -16,6 +16,9 @@ Fixtures:
   csr.npz       F6  canonical CSR + PatternMapper (crow, col) for the F3 and F5 graphs
   geostats.npz  F7  reference compute_geometry_statistics (statistics.py:20-83): 150 reaches x 31 and
                     x 30 days (odd / even median), NaN discharge entries, default and mock bounds
+  collate.npz   F9  per-batch gauge union: reference builders.construct_network_matrix + the network
+                    half of Merit._collate_gages (merit.py:197-238) on a synthetic 3k-reach CONUS with
+                    12 gauge subsets (nested gauges, a headwater gauge, a gauge missing from the store)
   daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
                     downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
                     warmup 3, and torch autograd's d loss / d runoff
@@ -230,10 +233,125 @@ def make_daily():
                         ref_grad=runoff.grad.numpy())
 
 
+def make_collate():
+    """F9: the reference's batch collation on synthetic gauge subsets (builders.py:55-109,
+    merit.py:197-238).  builders.py / merit.py import rustworkx, xarray, zarr and the ddr package at
+    module level; none of those names is used by the two functions run here, so they are stub modules.
+    The subsets store is a dict of objects with the zarr group interface the functions use
+    (``group[name][:]``, ``.attrs``, ``.keys()``)."""
+    load_reference()
+    for name in ["rustworkx", "xarray", "zarr", "zarr.storage", "ddr.geodatazoo", "ddr.io",
+                 "ddr.geodatazoo.base_geodataset", "ddr.geodatazoo.dataclasses", "ddr.io.readers",
+                 "ddr.io.statistics", "ddr.validation.enums"]:
+        m = types.ModuleType(name)
+        m.__path__ = []
+        sys.modules[name] = m
+    sys.modules["zarr"].Group = object
+    sys.modules["rustworkx"].PyDiGraph = object
+    sys.modules["zarr"].storage = sys.modules["zarr.storage"]
+    sys.modules["xarray"].Dataset = object
+    sys.modules["ddr.geodatazoo.base_geodataset"].BaseGeoDataset = object
+    sys.modules["ddr.geodatazoo.dataclasses"].Dates = object
+    sys.modules["ddr.geodatazoo.dataclasses"].RoutingDataclass = object
+    for f in ["IcechunkUSGSReader", "build_flow_scale_tensor", "fill_nans", "filter_gages_by_area_threshold",
+              "filter_gages_by_da_valid", "filter_headwater_gages", "naninfmean", "read_zarr"]:
+        setattr(sys.modules["ddr.io.readers"], f, None)
+    sys.modules["ddr.io.statistics"].set_statistics = None
+    sys.modules["ddr.validation.enums"].Mode = object
+
+    def _load(name, path):
+        spec = importlib.util.spec_from_file_location(name, path)
+        m = importlib.util.module_from_spec(spec)
+        sys.modules[name] = m
+        spec.loader.exec_module(m)
+        return m
+
+    builders = _load("ddr.io.builders", REF / "io/builders.py")
+    merit = _load("ddr.geodatazoo.merit", REF / "geodatazoo/merit.py")
+    captured = {}
+    merit.build_flow_scale_tensor = lambda **kw: None
+    merit.create_hydrofabric_observations = lambda **kw: None
+    merit.RoutingDataclass = lambda **kw: captured.update(kw)
+
+    net = synthetic.forest(synthetic.zipf_sizes(3000, 12, 0.35), seed=9, single_inflow=0.3)
+    down = net.down
+    n = net.n
+    rng = np.random.default_rng(9)
+    # upstream closure of a reach: every reach whose flow path passes through it (topological order:
+    # upstream reaches have lower ids, so one descending sweep marks them)
+    def upstream(x):
+        inside = np.zeros(n, bool)
+        inside[x] = True
+        for j in range(x - 1, -1, -1):
+            if down[j] >= 0 and inside[down[j]]:
+                inside[j] = True
+        inside[x] = False
+        return np.flatnonzero(inside)
+
+    outlets = np.flatnonzero(down < 0)
+    big = outlets[np.argsort(-net.basin_sizes)][:4]
+    gauges = list(big)
+    # nested gauges inside the largest basin, a headwater gauge, random interior gauges
+    up0 = upstream(big[0])
+    gauges += list(rng.choice(up0, 4, replace=False))
+    heads = np.setdiff1d(np.arange(n), down[down >= 0])
+    gauges.append(int(rng.choice(heads)))
+    gauges += list(rng.choice(np.flatnonzero(down >= 0), 3, replace=False))
+
+    class Sub:
+        def __init__(self, rows, cols, attrs):
+            self._a = {"indices_0": rows, "indices_1": cols}
+            self.attrs = attrs
+
+        def __getitem__(self, k):
+            return self._a[k]
+
+    store = {}
+    sub_rows, sub_cols, sub_off, gidx, ids = [], [], [0], [], []
+    for k, x in enumerate(gauges):
+        ups = upstream(int(x))
+        rows = down[ups].astype(np.int32)
+        cols = ups.astype(np.int32)
+        perm = rng.permutation(len(rows))  # the engine's subset order is arbitrary
+        rows, cols = rows[perm], cols[perm]
+        gid = f"{1000000 + k:08d}"
+        store[gid] = Sub(rows, cols, {"gage_idx": int(x), "gage_catchment": 70000 + k, "shape": [n, n]})
+        sub_rows.append(rows)
+        sub_cols.append(cols)
+        sub_off.append(sub_off[-1] + len(rows))
+        gidx.append(int(x))
+        ids.append(gid)
+
+    class Store(dict):
+        pass
+
+    st = Store(store)
+    batch = np.array(ids[:6] + ["09999999"] + ids[6:])  # one gauge missing from the store
+    coo, out_idx, out_wb = builders.construct_network_matrix([b for b in batch.tolist() if b in st], st)
+    self_ = SimpleNamespace(gages_adjacency=st, merit_ids=np.arange(n, dtype=np.int64) + 500000,
+                            obs_reader=SimpleNamespace(gage_dict={}), dates=None, observations=None,
+                            _build_common_tensors=lambda csr, ids_, act: (csr, None, None, {k: None for k in (
+                                "length", "slope", "side_slope", "top_width", "x")}))
+    merit.Merit._collate_gages(self_, batch)
+    csr = captured["adjacency_matrix"]
+    of = captured["outflow_idx"]
+    pairs = np.array(sorted(zip(coo.row.tolist(), coo.col.tolist())), dtype=np.int64).reshape(-1, 2)
+    np.savez_compressed(HERE / "collate.npz", n_conus=np.int64(n), conus_rows=net.rows, conus_cols=net.cols,
+                        sub_rows=np.concatenate(sub_rows), sub_cols=np.concatenate(sub_cols),
+                        sub_off=np.array(sub_off, np.int64), gage_idx=np.array(gidx, np.int64), gage_ids=np.array(ids),
+                        batch=batch, ref_union_pairs=pairs, ref_gage_idx=np.array(out_idx, np.int64),
+                        ref_gage_catchment=np.array(out_wb, np.int64),
+                        ref_divide_ids=np.asarray(captured["divide_ids"], np.int64),
+                        ref_crow=csr.indptr.astype(np.int64), ref_col=csr.indices.astype(np.int64),
+                        ref_outflow_flat=np.concatenate(of).astype(np.int64),
+                        ref_outflow_off=np.concatenate([[0], np.cumsum([len(o) for o in of])]).astype(np.int64),
+                        ref_gage_catchment_batch=np.array(captured["gage_catchment"], np.int64))
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
-            {"geostats": make_geostats, "daily": make_daily}[name]()
+            {"geostats": make_geostats, "daily": make_daily, "collate": make_collate}[name]()
         return
     torch.manual_seed(0)
     utils, mmc = load_reference()
