@@ -855,24 +855,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int e4 = t & 3;
       const R gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
       const R xtk = xc[k];
-      const ReachStatic<R> st = tab.template get<true>(rs);
+#ifndef DDR_BWD_EXACT
+#define DDR_BWD_EXACT 0
+#endif
+      const ReachStatic<R> st = tab.template get<!DDR_BWD_EXACT>(rs);
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
       const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
       const R gb = R(gb64);
       const R Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);     // Q_{t-1}
       R c1, c2, c3, gQ, gn, gq, gp;
-      if constexpr (std::is_same<R, float>::value) {
+      if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
         const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
         c1 = o.c1; c2 = o.c2; c3 = o.c3; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
       } else {
         const R qvk = static_cast<const R*>(a.qs)[xs_base + (int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale
         R c4, tw, ss;
         Geom<R> geo;
-        coefficients<R, true>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
+        coefficients<R, !DDR_BWD_EXACT>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
         const R qc = rmax(qvk, cs.qlb);
         const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
-        coefficients_vjp<R, true>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+        coefficients_vjp<R, !DDR_BWD_EXACT>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
       }
       if (active) {
         pn[k] = pn[k] + gn;

@@ -19,6 +19,8 @@ Fixtures:
   collate.npz   F9  per-batch gauge union: reference builders.construct_network_matrix + the network
                     half of Merit._collate_gages (merit.py:197-238) on a synthetic 3k-reach CONUS with
                     12 gauge subsets (nested gauges, a headwater gauge, a gauge missing from the store)
+  deep.npz      F10 the reference on C5's 281k-reach, 2215-deep basin over 24 h: unit-parameter
+                    gradients and the outlet series (fp32 gradient accuracy along deep chains)
   daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
                     downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
                     warmup 3, and torch autograd's d loss / d runoff
@@ -348,10 +350,34 @@ def make_collate():
                         ref_gage_catchment_batch=np.array(captured["gage_catchment"], np.int64))
 
 
+def deep_case(T=24):
+    """The C5 forest's largest basin (281k reaches, depth 2215), routed alone (tests/conftest.py)."""
+    sys.path.insert(0, str(HERE.parent))
+    from conftest import deep_case as _deep
+
+    return _deep(T)
+
+
+def make_deep():
+    """F10: the reference (fp32 elementwise + SciPy fp64 solve, torch autograd) on the 281k-reach,
+    2215-deep basin of C5 over 24 hours: unit-parameter gradients of sum(W * runoff) and the outlet
+    series.  Pins what fp32 arithmetic itself does to gradients along a 2215-hop chain."""
+    import time
+
+    _, mmc = load_reference()
+    c = deep_case()
+    dc = routing_dc(c.n, c.rows, c.cols, c.attrs)
+    t0 = time.time()
+    res, _ = run_ref(mmc, PARAMS_DEFAULT, dc, c.qprime, c.u, c.W)
+    print(f"deep: reference fwd+bwd {time.time() - t0:.0f}s", flush=True)
+    np.savez_compressed(HERE / "deep.npz", T=np.int64(c.qprime.shape[0]), n=np.int64(c.n),
+                        ref_outlet=res["runoff"][c.n - 1], **{f"ref_{k}": v for k, v in res.items() if k.startswith("grad_")})
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
-            {"geostats": make_geostats, "daily": make_daily, "collate": make_collate}[name]()
+            {"geostats": make_geostats, "daily": make_daily, "collate": make_collate, "deep": make_deep}[name]()
         return
     torch.manual_seed(0)
     utils, mmc = load_reference()

@@ -147,6 +147,88 @@ def test_c5_small_basins_match_oracle_with_gradients(c5):
         assert normrel(c5.out[k][sel].cpu().numpy(), ref["grads"][rk]) <= 5e-5, k
 
 
+def test_c5_giant_basin_oracle_and_partition_invariance(c5):
+    """The 281k-reach basin (0.35 N, depth 2215): the longest chain of inter-workgroup hand-offs.
+    (1) Routed alone over the first 72 hours, its discharge matches the oracle.  (2) Over the full
+    8760 h, routed alone under two other partitions (the basin's own default packing, and 1024-reach
+    workgroups), discharge and gradients are bitwise those of the basin inside the 800k forest.
+    Gradient accuracy along this chain is pinned against the reference by test_deep_basin_gradients."""
+    members, nblk = _basins_by_blocks(c5)
+    b = int(np.argmax([len(m) for m in members]))
+    ids = np.sort(members[b])
+    assert len(ids) > 250_000 and nblk[b] >= 50
+    ns, rs, cs = c5.basin(ids)
+    sel = torch.from_numpy(ids).to(c5.dev)
+    Ts = 72
+    short = FullForest.__new__(FullForest)
+    short.net, short.T, short.dev = c5.net, Ts, c5.dev
+    short.n, short.q, short.p, short.length, short.slope, short.x = c5.n, c5.q, c5.p, c5.length, c5.slope, c5.x
+    short.qprime = c5.qprime[:Ts].contiguous()
+    short.W = c5.W[:, :Ts].contiguous()
+    got = short.run(RiverGraph(ns, rs, cs, steps_hint=Ts), ids)
+    ref = short.oracle(ids, grads=False)
+    assert maxrel(got["runoff"].cpu().numpy(), ref["runoff"]) <= 1e-6
+    del short, got
+    full = c5.out["runoff"][sel].cpu().numpy()
+    for gkw in ({}, {"max_block_reaches": 1024}):
+        g = RiverGraph(ns, rs, cs, **gkw)
+        assert g.info.n_cut > 0
+        alone = c5.run(g, ids)
+        np.testing.assert_array_equal(alone["runoff"].cpu().numpy(), full)
+        for k in ("gn", "gq", "gp"):
+            np.testing.assert_array_equal(alone[k].cpu().numpy(), c5.out[k][sel].cpu().numpy())
+        del alone, g
+        torch.cuda.empty_cache()
+
+
+def test_deep_basin_gradients_vs_reference(cuda):
+    """Gradients along a 2215-hop chain (tests/golden/deep.npz: the reference itself on C5's 281k-reach
+    basin over 24 h).  fp32 rounding accumulates along the chain in ANY fp32 adjoint: the reference's
+    own gradients are 2.6e-3 / 7.9e-3 / 4.3e-3 (norm-rel, n / q / p) from the fp64 adjoint here.  The
+    bar: the fp32 kernel is at least as close to the fp64 oracle as the reference, its discharge is
+    within the north star's 1e-4 of the reference, and the fp64 kernel agrees with the fp64 oracle to
+    1e-10 (the algorithm is exact)."""
+    from conftest import deep_case, load_golden
+
+    d = load_golden("deep")
+    c = deep_case(int(d["T"]))
+    rngs = RANGES
+    net = O.Network.from_coo(c.n, c.rows, c.cols)
+    tt = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(cuda, dt)  # noqa: E731
+    res = {}
+    for dt in (torch.float32, torch.float64):
+        u = {k: tt(c.u[k], dt).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial")}
+        n = u["n"] * (rngs["n"][1] - rngs["n"][0]) + rngs["n"][0]
+        q = u["q_spatial"] * (rngs["q_spatial"][1] - rngs["q_spatial"][0]) + rngs["q_spatial"][0]
+        lo, hi = np.log(rngs["p_spatial"][0] + 1e-6), np.log(rngs["p_spatial"][1])
+        p = torch.exp(u["p_spatial"] * (hi - lo) + lo)
+        slope = torch.clamp(tt(c.attrs.slope, dt), min=1e-3)
+        g = RiverGraph(c.n, c.rows, c.cols, steps_hint=int(d["T"]))
+        runoff, _, _, _ = route(g, tt(c.qprime, dt), n, q, p, tt(c.attrs.length, dt), slope, tt(c.attrs.x, dt),
+                                consts=RouteConsts())
+        runoff.backward(tt(c.W, dt))
+        torch.cuda.synchronize()
+        res[dt] = {"outlet": runoff[c.n - 1].detach().cpu().numpy(),
+                   **{k: v.grad.cpu().numpy().astype(np.float64) for k, v in u.items()},
+                   "reaches": O.Reaches(n.detach().cpu().numpy(), q.detach().cpu().numpy(), p.detach().cpu().numpy(),
+                                        c.attrs.length.astype(np.float64 if dt == torch.float64 else np.float32),
+                                        slope.cpu().numpy(), c.attrs.x.astype(np.float64 if dt == torch.float64 else np.float32))}
+    assert maxrel(res[torch.float32]["outlet"], d["ref_outlet"]) <= 1e-4
+    r64 = res[torch.float64]["reaches"]
+    qp64 = c.qprime.astype(np.float64)
+    f64 = O.route(net, r64, qp64, O.Bounds(), dtype=np.float64)
+    bw = O.route_backward(net, r64, qp64, f64["x"], c.W.astype(np.float64), O.Bounds())
+    u64 = {k: c.u[k].astype(np.float64) for k in c.u}
+    g64 = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], u64["n"], u64["q_spatial"],
+                                  u64["p_spatial"], rngs)
+    for k in ("n", "q_spatial", "p_spatial"):
+        assert normrel(res[torch.float64][k], g64[k]) <= 1e-10, k
+        ref_err = normrel(d[f"ref_grad_{k}"], g64[k])
+        ours = normrel(res[torch.float32][k], g64[k])
+        assert ours <= ref_err, (k, ours, ref_err)
+        assert normrel(res[torch.float32][k], d[f"ref_grad_{k}"]) <= 2.5 * ref_err, k
+
+
 def test_c5_outputs_finite_and_bounded(c5):
     r = c5.out["runoff"]
     assert r.shape == (800_000, T_FULL)
