@@ -203,7 +203,9 @@ def test_deep_basin_gradients_vs_reference(cuda):
         lo, hi = np.log(rngs["p_spatial"][0] + 1e-6), np.log(rngs["p_spatial"][1])
         p = torch.exp(u["p_spatial"] * (hi - lo) + lo)
         slope = torch.clamp(tt(c.attrs.slope, dt), min=1e-3)
-        g = RiverGraph(c.n, c.rows, c.cols, steps_hint=int(d["T"]))
+        # fp64 statics and slots take twice the LDS: smaller workgroups
+        g = RiverGraph(c.n, c.rows, c.cols, steps_hint=int(d["T"]),
+                       max_block_reaches=1024 if dt == torch.float64 else 0)
         runoff, _, _, _ = route(g, tt(c.qprime, dt), n, q, p, tt(c.attrs.length, dt), slope, tt(c.attrs.x, dt),
                                 consts=RouteConsts())
         runoff.backward(tt(c.W, dt))
