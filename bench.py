@@ -7,7 +7,7 @@ Workloads (``--workload``; the default is the headline metric):
   stems, 35 % single-inflow reaches), loss = sum(W * runoff).  One step = one full forward (hot start +
   8759 routing steps) and one full adjoint (gradients w.r.t. n, q_spatial, p_spatial).
 * ``c3`` -- the training batch: 256 gauged subnetworks (log-uniform 100..20k reaches), rho = 90 days
-  (T = 2136 h), one gauge per subnetwork outlet.  One step = parameter network forward (a KAN
+  (T = 2136 h) from a daily q' store (the reference default), one gauge per subnetwork outlet.  One step = parameter network forward (a KAN
   stand-in: pykan is not installed here) -> denormalize -> fused gauge-mode routing with the daily
   objective (trim [13 : -11 + tau], area pooling) -> L1 loss vs synthetic observations -> backward ->
   RCCL all-reduce of the network's gradients -> clip + Adam step (scripts/train.py:54-104).
@@ -217,7 +217,11 @@ def main():
     u = synthetic.unit_parameters(net.n, 11)
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a)[ids])).to(dev)  # noqa: E731
     length, slope, xs = tt(at.length), tt(np.maximum(at.slope, np.float32(1e-3))), tt(at.x)
-    qprime = synthetic.lateral_inflow_torch(net.n, T, seed=11, device=dev, ids=ids)
+    # C3 trains from a DAILY q' store (the reference's default, configs.py:61-65 is_hourly=False):
+    # (ceil(T / 24), N) rows indexed q'[t // 24] in the gather, the reader's repeat(24)
+    # (readers.py:513-519); the other workloads route an hourly (T, N) field
+    qp_hours = 24 if args.workload == "c3" else 1
+    qprime = synthetic.lateral_inflow_torch(net.n, -(-T // qp_hours), seed=11, device=dev, ids=ids)
     consts = RouteConsts()
     lib = _lib.load()
     lib_hash = lib.ddr_version().decode().split()[-1]
@@ -257,7 +261,7 @@ def main():
             un = model(feats)
             n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
             daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
-                                   fast_math=args.fast_math)
+                                   fast_math=args.fast_math, steps=T, qprime_hours=qp_hours)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
             loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
             loss.backward()
@@ -358,7 +362,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T,
+            "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T, "qprime_store": "daily" if qp_hours == 24 else "hourly",
                        "forward_math": "fast (hardware rcp/log/exp fp32)" if args.fast_math else "exact (reference op order)",
                        "basins": int(len(net.basin_sizes)), "largest_basin": largest,
                        "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
@@ -407,7 +411,7 @@ def time_training_stream(args, dev):
         outlets = np.flatnonzero(nt.down < 0)
         data.append(dict(net=nt, length=tt(at.length), slope=tt(np.maximum(at.slope, np.float32(1e-3))), xs=tt(at.x),
                          feats=tt(synthetic.reach_features(nt.n, seed=200 + k)),
-                         qprime=synthetic.lateral_inflow_torch(nt.n, T, seed=200 + k, device=dev),
+                         qprime=synthetic.lateral_inflow_torch(nt.n, -(-T // 24), seed=200 + k, device=dev),
                          gz=GaugeMap.build([np.array([o]) for o in outlets], nt.n, dev),
                          obs=torch.from_numpy(np.random.default_rng(300 + k).lognormal(np.log(5.0), 1.0,
                                               (len(outlets), window.D)).astype(np.float32)).to(dev)))
@@ -435,7 +439,7 @@ def time_training_stream(args, dev):
         un = model(d["feats"])
         n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
         daily, _, _, _ = route(g, d["qprime"], n, q, p, d["length"], d["slope"], d["xs"], gauges=d["gz"],
-                               daily=window, consts=consts)
+                               daily=window, consts=consts, steps=T, qprime_hours=24)
         loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])
         loss.backward()
         allreduce_gradients(list(model.parameters()))
@@ -486,8 +490,22 @@ def time_dropin(args, net, at, u, qprime, W, dev):
         one()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.dropin_steps * 1e3
+    # the BMI update (ddr_bmi.py:285-305): one route_timestep per hour under no_grad, state carried
+    eng = model.routing_engine
+    K = 24
+    with torch.no_grad():
+        for i in range(K + 2):
+            if i == 2:
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+            qc = torch.clamp(qprime[i % qprime.shape[0]], min=1e-4)
+            eng._discharge_t = eng.route_timestep(q_prime_clamp=qc)
+        torch.cuda.synchronize()
+    bmi_ms = (time.perf_counter() - t1) / K * 1e3
     return {"ms_per_step": ms, "steps": args.dropin_steps,
-            "note": "dmc() forward + backward incl. setup_inputs (cached graph, hot start, PatternMapper)"}
+            "note": "dmc() forward + backward incl. setup_inputs (cached graph, hot start, PatternMapper)",
+            "route_timestep_ms": bmi_ms,
+            "route_timestep_note": f"BMI update: one MuskingumCunge.route_timestep (one hour, {net.n} reaches, no_grad), mean of {K}"}
 
 
 def block_profile(path, g, step, lib):

@@ -184,7 +184,10 @@ class MuskingumCunge:
         if carry_state and self._discharge_t is not None:
             return
         assert self.q_prime is not None, "q_prime must be set before initializing discharge state"
-        assert ~torch.any(torch.isnan(self.q_prime)), "q_prime has NaN flows"
+        # mmc.py:335 -- one reduction pass over q' (a NaN makes the sum NaN); the elementwise check
+        # (which materialises a (T, N) mask) only decides the rare NaN-sum case (+inf and -inf)
+        if bool(torch.isnan(self.q_prime.sum())):
+            assert ~torch.any(torch.isnan(self.q_prime)), "q_prime has NaN flows"
         mapper, _, _ = self.create_pattern_mapper()
         self._discharge_t = compute_hotstart_discharge(self.q_prime[0].to(self.device), mapper, self.discharge_lb,
                                                        self.device)

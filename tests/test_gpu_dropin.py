@@ -181,3 +181,19 @@ def test_triangular_solve_routing_matrix(cuda):
     x = triangular_sparse_solve(mapper.map(c1_), mapper.crow_indices, mapper.col_indices, b, True, False, cuda)
     ref = O.Network.from_coo(net.n, net.rows, net.cols).lower_solve(c1.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_array_equal(x.cpu().numpy(), ref.astype(np.float32))
+
+
+def test_nan_streamflow_asserts_like_the_reference(cuda):
+    """mmc.py:335: a NaN anywhere in q' fails setup with "q_prime has NaN flows"; +inf and -inf
+    together (a NaN sum but no NaN element) do not."""
+    case, _ = golden_case("tree300", PARAMS_DEFAULT)
+    sp_params = {k: torch.from_numpy(v).to(cuda) for k, v in case.u.items()}
+    q = torch.from_numpy(case.qprime).clone()
+    q[7, 11] = float("nan")
+    model = dmc(cfg_of(PARAMS_DEFAULT), device=cuda)
+    with pytest.raises(AssertionError, match="NaN flows"):
+        model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params)
+    q = torch.from_numpy(case.qprime).clone()
+    q[5, 3], q[6, 4] = float("inf"), float("-inf")
+    mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
+    mc.setup_inputs(golden_dataclass(case), q, sp_params)  # no assertion
