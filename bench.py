@@ -181,8 +181,11 @@ def main():
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
     ap.add_argument("--stream-workers", type=int, default=4)
     ap.add_argument("--fast-math", action="store_true",
-                    help="forward coefficients in hardware-approximate fp32 math (route(fast_math=True))")
+                    help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
+    ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
+                    help="forward coefficient arithmetic (default faithful, the drop-in's default; --fast-math = fast)")
     args = ap.parse_args()
+    args.math = args.math or ("fast" if args.fast_math else "faithful")
     spec = WORKLOADS[args.workload]
     T = args.T or spec["T"]
     args.T = T
@@ -237,7 +240,7 @@ def main():
             for t_ in (u_n, u_q, u_p):
                 t_.grad = None
             n, q, p = denorm(u_n, u_q, u_p)
-            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, fast_math=args.fast_math)
+            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, math=args.math)
             runoff.backward(W)
 
     elif args.workload == "c3":
@@ -261,7 +264,7 @@ def main():
             un = model(feats)
             n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
             daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
-                                   fast_math=args.fast_math, steps=T, qprime_hours=qp_hours)
+                                   math=args.math, steps=T, qprime_hours=qp_hours)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
             loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
             loss.backward()
@@ -278,7 +281,7 @@ def main():
             with torch.no_grad():
                 if args.workload == "c4":  # first: the kernel timer reports the last forward launch
                     geometry_statistics_from_inflow(g, qprime[::24][:365], n, p, q, slope)
-                route(g, qprime, n, q, p, length, slope, xs, consts=consts, save=False, fast_math=args.fast_math)
+                route(g, qprime, n, q, p, length, slope, xs, consts=consts, save=False, math=args.math)
 
     ev = []
     kms = {"forward": [], "backward": []}  # main routing kernels, HIP events on the launch stream
@@ -363,7 +366,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T, "qprime_store": "daily" if qp_hours == 24 else "hourly",
-                       "forward_math": "fast (hardware rcp/log/exp fp32)" if args.fast_math else "exact (reference op order)",
+                       "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",
+                                        "faithful": "faithful (reference op order, IEEE division, fp32 faithful-class pow)",
+                                        "fast": "fast (hardware rcp/log/exp fp32)"}[args.math],
                        "basins": int(len(net.basin_sizes)), "largest_basin": largest,
                        "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
                        "cut_edges_rank0": g.info.n_cut, "generations_rank0": g.info.generations,

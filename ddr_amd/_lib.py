@@ -37,6 +37,7 @@ DDR_FWD_CARRY = 2
 DDR_FWD_NO_RUNOFF = 4
 DDR_FWD_ACCUMULATE = 8
 DDR_FWD_FAST_MATH = 16
+DDR_FWD_FAITHFUL_MATH = 32
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 

@@ -107,6 +107,26 @@ __device__ __forceinline__ float pow_pos(float x, float y, double* ln_out = null
   return (float)exp_tab((double)y * l, K);
 }
 
+// x^y for x > 0 normal, |y log2 x| < 126, in fp32 arithmetic only (no fp64, no tables): a
+// faithful-class pow like the reference's Sleef powf_u10.  x = 2^e m with m in [sqrt(1/2), sqrt(2)),
+// so the hardware log2 of m is small and its absolute error tiny; y (e + log2 m) is carried as an
+// exact product split (FMA remainders), its integer part goes to the exponent and only the fraction
+// (|f| <~ 1) meets v_exp_f32.  Measured against the correctly rounded value: tools/pow_check.hip.
+__device__ __forceinline__ float pow_faithful(float x, float y) {
+  const int u = __float_as_int(x);
+  const int ei = (u - 0x3F3504F3) >> 23;
+  const float m = __int_as_float(u - (ei << 23));
+  const float l = __builtin_amdgcn_logf(m);
+  const float fe = (float)ei;
+  const float p = y * fe;
+  const float pe = fmaf(y, fe, -p);
+  const float q = y * l;
+  const float qe = fmaf(y, l, -q);
+  const float ip = __builtin_rintf(p);
+  const float f = ((p - ip) + q) + (pe + qe);
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)ip);
+}
+
 // ---- lockstep forms: NP independent evaluations advanced one operation at a time, so a wave
 // carries NP dependency chains at once (the routing ticks are latency-bound at 4 waves/SIMD) ----
 #define DDR_FOR_NP _Pragma("unroll") for (int h = 0; h < NP; ++h)

@@ -297,6 +297,33 @@ __device__ __forceinline__ PhysOut<float> coefficients_fast(const ReachStatic<fl
   return o;
 }
 
+// The reference's operation sequence (coefficients_np) with IEEE divisions (div_rn) and square
+// root, and the pows in fp32 faithful-class arithmetic (pow_faithful) instead of fp64: no fp64
+// instruction and no table lookup on the forward's dependency chain.
+__device__ __forceinline__ PhysOut<float> coefficients_faithful(const ReachStatic<float>& s, float Q,
+                                                                const Consts<float>& c) {
+  PhysOut<float> o;
+  const float ratio = div_rn((Q * s.n) * s.qe1(), s.dd);
+  const float depth = rmax(pow_faithful(ratio, s.expo), c.dlb);
+  const float dq = pow_faithful(depth, s.qe);
+  o.tw = s.p * dq;
+  const float ssr = div_rn(o.tw * s.qe, 2.0f * depth);
+  o.ss = rclamp(ssr, c.sslb, c.ssub);
+  const float bw = rmax(o.tw - (2.0f * o.ss) * depth, c.bwlb);
+  const float area = ((o.tw + bw) * depth) * 0.5f;
+  const float wp = bw + (2.0f * depth) * sqrtf(1.0f + o.ss * o.ss);
+  const float Rh = div_rn(area, wp);
+  const float r23 = pow_faithful(Rh, two_thirds<float>());
+  const float cel = div_rn(rclamp((s.inv_n * r23) * s.sqrtS, c.vlb, c.vub) * 5.0f, 3.0f);
+  const float twok = 2.0f * div_rn(s.L, cel);
+  const float den = (twok * s.omX()) + c.dt;
+  o.c1 = div_rn(c.dt - twok * s.X, den);
+  o.c2 = div_rn(c.dt + twok * s.X, den);
+  o.c3 = div_rn((twok * s.omX()) - c.dt, den);
+  o.c4 = div_rn(2.0f * c.dt, den);
+  return o;
+}
+
 // VJP of (c1, c2, c3, c4) w.r.t. (Q, n, q_spatial, p_spatial) at the point described by g.
 template <typename R, bool Fast = false>
 __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, const Consts<R>& c,

@@ -312,7 +312,9 @@ struct StatTab {
 // (coefficients_fast, the operation set of the adjoint's recompute) instead of the reference's exact
 // operation sequence; ~1e-6 relative per coefficient, and few enough registers that all of a
 // thread's slices run their physics in lockstep.
-template <typename R, int KR, bool FM>
+// MATH: 0 exact (reference op order, correctly rounded pow), 1 fast (DDR_FWD_FAST_MATH), 2 faithful
+// (DDR_FWD_FAITHFUL_MATH: exact op order and IEEE divisions, fp32 faithful-class pow).
+template <typename R, int KR, int MATH>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
 #ifndef DDR_FWD_NP
@@ -321,7 +323,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #ifndef DDR_FWD_NP_FAST
 #define DDR_FWD_NP_FAST 1
 #endif
-  constexpr bool kFast = FM && std::is_same<R, float>::value;
+  constexpr bool kFast = MATH == 1 && std::is_same<R, float>::value;
+  constexpr bool kFaith = MATH == 2 && std::is_same<R, float>::value;
   constexpr int NPW = kFast ? DDR_FWD_NP_FAST : DDR_FWD_NP;
   constexpr int NP = KR < NPW ? KR : NPW;  // slices whose physics runs in lockstep
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -336,7 +339,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
-  const Consts<R> cs = consts_of<R>(a, !kFast);
+  const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool accum = a.flags & DDR_FWD_ACCUMULATE;  // every step a hot start (daily accumulation)
@@ -460,6 +463,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if constexpr (kFast) {
 #pragma unroll
           for (int h = 0; h < NP; ++h) ph[h] = coefficients_fast(st[h], Qv[h], cs);
+        } else if constexpr (kFaith) {
+#pragma unroll
+          for (int h = 0; h < NP; ++h) ph[h] = coefficients_faithful(st[h], Qv[h], cs);
         } else {
           coefficients_np<R, NP>(st, Qv, cs, ph);
         }
@@ -1138,9 +1144,11 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
     hipLaunchKernelGGL(finish_grads_kernel<R>, dim3(fb), dim3(256), 0, stream, g->n,
                        (const double*)(a.bwd_bnd + 2 * g->n_cut * a.T), (R*)a.gn, (R*)a.gq, (R*)a.gp);
   } else {
-    auto kern = route_forward_kernel<R, KR, false>;
-    if constexpr (std::is_same<R, float>::value)
-      if (a.flags & DDR_FWD_FAST_MATH) kern = route_forward_kernel<R, KR, true>;
+    auto kern = route_forward_kernel<R, KR, 0>;
+    if constexpr (std::is_same<R, float>::value) {
+      if (a.flags & DDR_FWD_FAST_MATH) kern = route_forward_kernel<R, KR, 1>;
+      else if (a.flags & DDR_FWD_FAITHFUL_MATH) kern = route_forward_kernel<R, KR, 2>;
+    }
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
@@ -1163,9 +1171,9 @@ int max_resident_blocks(const Graph* g, bool backward) {
   const size_t smem = route_smem_bytes<R>(g, backward);
   const void* f = nullptr;
   switch (g->kr) {
-    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1, false>; break;
-    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2, false>; break;
-    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4, false>;
+    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1, 0>; break;
+    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2, 0>; break;
+    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4, 0>;
   }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;

@@ -342,8 +342,13 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
           q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
           save: bool | None = None, steps: int | None = None, qprime_hours: int = 1,
           qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False,
-          fast_math: bool = False):
+          fast_math: bool = False, math: str | None = None):
     """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last).
+
+    ``math`` (fp32 forward): ``"exact"`` (default) -- the reference's operation order, IEEE division,
+    correctly rounded pow: bit-identical to the oracle; ``"faithful"`` -- the same order and IEEE
+    divisions with the pows in fp32 faithful-class arithmetic (the accuracy class of the reference's
+    own Sleef ``powf``; no fp64 on the dependency chain); ``"fast"`` (= ``fast_math=True``).
 
     ``fast_math`` (fp32): the forward's Muskingum coefficients in hardware-approximate fp32 math
     (v_rcp / v_log / v_exp, the adjoint's operation set) instead of the reference's exact operation
@@ -367,8 +372,12 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
         steps = qprime.shape[0] * max(1, qprime_hours)
     if save is None:
         save = (not accumulate) and torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
+    math = math or ("fast" if fast_math else "exact")
+    if math not in ("exact", "faithful", "fast"):
+        raise ValueError(f"math must be 'exact', 'faithful' or 'fast', not {math!r}")
     flags = ((_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
-             | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0) | (_lib.DDR_FWD_FAST_MATH if fast_math else 0))
+             | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0) | (_lib.DDR_FWD_FAST_MATH if math == "fast" else 0)
+             | (_lib.DDR_FWD_FAITHFUL_MATH if math == "faithful" else 0))
     valid = None if qprime_valid is None else qprime_valid.to(device=dev, dtype=torch.uint8).contiguous()
     gid = register_graph(graph)
     gz = gauges

@@ -12,6 +12,8 @@ The hot start (``compute_hotstart_discharge``, mmc.py:25-66) and the single-step
 
 from __future__ import annotations
 
+import os
+
 import logging
 import weakref
 from typing import Any
@@ -93,6 +95,11 @@ class MuskingumCunge:
     def __init__(self, cfg: Any, device: str | torch.device = "cpu") -> None:
         self.cfg = cfg
         self.device = device
+        # forward coefficient arithmetic of the fused kernel (ops.route ``math``): "faithful" (default:
+        # the reference's operation order and IEEE divisions, pows in fp32 faithful-class arithmetic --
+        # the accuracy class of the reference's own Sleef powf), "exact" (correctly rounded pow:
+        # bit-identical to the oracle) or "fast"; cfg.params.routing_math or DDR_ROUTING_MATH override
+        self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "faithful")
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None
@@ -226,7 +233,7 @@ class MuskingumCunge:
         qp = self.q_prime.to(torch.float32)
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
                                        self.slope, self.x_storage, q0=self._discharge_t, gauges=self._gauges,
-                                       consts=self._consts())
+                                       consts=self._consts(), math=self.math)
         self._discharge_t = q_last
         if qp.shape[0] > 1:
             self.top_width = _apply_data_override(tw, self._data_top_width)
@@ -266,7 +273,8 @@ class MuskingumCunge:
         q = q_prime_clamp.to(torch.float32).reshape(1, -1)
         qp = torch.cat([q, q], 0)
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
-                                       self.slope, self.x_storage, q0=self._discharge_t, consts=self._consts())
+                                       self.slope, self.x_storage, q0=self._discharge_t, consts=self._consts(),
+                                       math=self.math)
         self.top_width = _apply_data_override(tw, self._data_top_width)
         self.side_slope = _apply_data_override(ss, self._data_side_slope)
         return q_last

@@ -167,7 +167,13 @@ typedef struct {
  * DDR_FWD_ACCUMULATE: every step is a hot start, Q_t = max((I - N)^-1 q'_t, q_lb) with step t
  * reading q' row t -- the per-day discharge accumulation of scripts/geometry_predictor.py:193-212
  * (compute_hotstart_discharge, mmc.py:25-66) for all days in one launch. */
-enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8, DDR_FWD_FAST_MATH = 16 };
+/* Forward coefficient arithmetic (fp32 only; default: the reference's operation order with IEEE
+ * division and a correctly rounded pow -- bit-identical to the oracle):
+ * DDR_FWD_FAITHFUL_MATH: the same operation order and IEEE divisions, pow in fp32 faithful-class
+ *   arithmetic (like the reference's own Sleef powf; no fp64 on the chain);
+ * DDR_FWD_FAST_MATH: hardware v_rcp / v_log / v_exp throughout (~1e-6 relative per coefficient). */
+enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8, DDR_FWD_FAST_MATH = 16,
+       DDR_FWD_FAITHFUL_MATH = 32 };
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
  * Returns DDR_ERR_TIMEOUT instead of launching when an earlier launch's hand-off timed out

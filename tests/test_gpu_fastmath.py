@@ -1,7 +1,9 @@
-"""The fast-math forward (route(fast_math=True), DDR_FWD_FAST_MATH): the Muskingum coefficients in
-hardware-approximate fp32 math (v_rcp / v_log / v_exp / v_rsq) instead of the reference's exact
-operation sequence.  It is not bit-identical to the oracle; it is held to the north star's stated
-fp32 tolerance (BASELINE.json: max rel err <= 1e-4 vs the reference fp32) on
+"""The approximate-math forwards: route(math="fast") (DDR_FWD_FAST_MATH: the Muskingum coefficients in
+hardware-approximate fp32 math, v_rcp / v_log / v_exp / v_rsq) and route(math="faithful")
+(DDR_FWD_FAITHFUL_MATH: the reference's operation sequence with IEEE divisions and the pows in fp32
+faithful-class arithmetic, like the reference's own Sleef powf).  Neither is bit-identical to the
+oracle; both are held to the north star's stated fp32 tolerance (BASELINE.json: max rel err <= 1e-4 vs
+the reference fp32) on
 
 * the reference's own golden outputs (tests/golden, made by running the reference),
 * the fp32 oracle (same inputs, exact recipe),
@@ -29,9 +31,10 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-4  # north star: max rel err vs the reference fp32
 GOLDEN = [("sandbox", PARAMS_MOCK), ("tree300", PARAMS_DEFAULT), ("c1", PARAMS_DEFAULT)]
+MODES = ["fast", "faithful"]
 
 
-def _run(case, dev, fast, gkw=None):
+def _run(case, dev, math, gkw=None):
     rng = case.params["parameter_ranges"]
     ls = case.params["log_space_parameters"]
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, torch.float32)  # noqa: E731
@@ -43,7 +46,7 @@ def _run(case, dev, fast, gkw=None):
     slope = torch.clamp(tt(case.slope), min=case.params["attribute_minimums"]["slope"])
     g = RiverGraph(case.n, case.rows, case.cols, **(gkw or {}))
     runoff, q_last, tw, ss = route(g, tt(case.qprime), n, q, p, tt(case.length), slope, tt(case.x),
-                                   consts=consts_of(case), fast_math=fast)
+                                   consts=consts_of(case), math=math)
     runoff.backward(tt(case.W))
     out = {"runoff": runoff.detach().cpu().numpy(), "q_last": q_last.detach().cpu().numpy(),
            "top_width": tw.detach().cpu().numpy(), "side_slope": ss.detach().cpu().numpy(),
@@ -56,13 +59,16 @@ def _run(case, dev, fast, gkw=None):
     return out
 
 
+@pytest.mark.parametrize("math", MODES)
 @pytest.mark.parametrize("name,params", GOLDEN, ids=[g[0] for g in GOLDEN])
 @pytest.mark.parametrize("gkw", [None, {"max_block_reaches": 64, "target_blocks": 1 << 20}], ids=["whole", "cut"])
-def test_fast_math_matches_reference_golden(cuda, name, params, gkw):
+def test_fast_math_matches_reference_golden(cuda, name, params, gkw, math):
     case, d = golden_case(name, params)
-    res = _run(case, cuda, True, gkw)
+    res = _run(case, cuda, math, gkw)
     if "ref_runoff" in d:
-        assert maxrel(res["runoff"], d["ref_runoff"]) <= TOL
+        err = maxrel(res["runoff"], d["ref_runoff"])
+        print(f"{name} {math}: forward vs reference golden max-rel {err:.2e}")
+        assert err <= TOL
     else:
         assert maxrel(res["runoff"][d["sample"]], d["ref_runoff_sample"]) <= TOL
         assert maxrel(res["runoff"][-1], d["ref_outlet"]) <= TOL
@@ -73,14 +79,15 @@ def test_fast_math_matches_reference_golden(cuda, name, params, gkw):
             assert normrel(res[f"grad_{k}"], d[f"ref_grad_{k}"]) <= 5e-5, k
 
 
+@pytest.mark.parametrize("math", MODES)
 @pytest.mark.parametrize("name,params", GOLDEN, ids=[g[0] for g in GOLDEN])
-def test_fast_math_vs_oracle_and_exact_kernel(cuda, name, params):
+def test_fast_math_vs_oracle_and_exact_kernel(cuda, name, params, math):
     case, _ = golden_case(name, params)
-    fast = _run(case, cuda, True)
-    exact = _run(case, cuda, False)
+    fast = _run(case, cuda, math)
+    exact = _run(case, cuda, "exact")
     ref = O.route(case.network(), fast["reaches"], case.qprime, case.bounds, dtype=np.float32)
     err = maxrel(fast["runoff"], ref["runoff"])
-    print(f"{name}: fast-math forward vs fp32 oracle max-rel {err:.2e}")
+    print(f"{name}: {math} forward vs fp32 oracle max-rel {err:.2e}")
     assert err <= TOL
     assert maxrel(fast["runoff"], exact["runoff"]) <= TOL
     for k in ("n", "q_spatial", "p_spatial"):
@@ -96,7 +103,8 @@ def _chunked_maxrel(a, b, rows=50_000):
     return m
 
 
-def test_fast_math_full_c5_within_tolerance_of_exact(cuda):
+@pytest.mark.parametrize("math", MODES)
+def test_fast_math_full_c5_within_tolerance_of_exact(cuda, math):
     """800k reaches x 8760 h: fast vs exact forward (itself bit-identical to the oracle), max-rel over
     all 7e9 values; gradients of a random linear loss norm-rel."""
     net = synthetic.forest(synthetic.zipf_sizes(800_000, 3000, 0.35), seed=5, single_inflow=0.35)
@@ -114,20 +122,21 @@ def test_fast_math_full_c5_within_tolerance_of_exact(cuda):
     gen = torch.Generator(device=cuda).manual_seed(77)
     W = torch.rand((net.n, T), device=cuda, generator=gen)
     outs = {}
-    for fast in (False, True):
+    for mode in ("exact", math):
         nt, qt, pt = (v.clone().requires_grad_(True) for v in (n, q, p))
-        runoff, _, _, _ = route(g, qp, nt, qt, pt, length, slope, x, consts=RouteConsts(), fast_math=fast)
+        runoff, _, _, _ = route(g, qp, nt, qt, pt, length, slope, x, consts=RouteConsts(), math=mode)
         runoff.backward(W)
-        outs[fast] = (runoff.detach(), nt.grad, qt.grad, pt.grad)
+        outs[mode] = (runoff.detach(), nt.grad, qt.grad, pt.grad)
         del runoff
-    err = _chunked_maxrel(outs[True][0], outs[False][0])
-    print(f"C5 full size: fast vs exact forward max-rel {err:.2e}")
+    err = _chunked_maxrel(outs[math][0], outs["exact"][0])
+    print(f"C5 full size: {math} vs exact forward max-rel {err:.2e}")
     assert err <= TOL
-    for a, b in zip(outs[True][1:], outs[False][1:]):
+    for a, b in zip(outs[math][1:], outs["exact"][1:]):
         assert normrel(a.cpu().numpy(), b.cpu().numpy()) <= 5e-5
 
 
-def test_fast_math_c3_daily_objective(cuda):
+@pytest.mark.parametrize("math", MODES)
+def test_fast_math_c3_daily_objective(cuda, math):
     """The C3 training objective (gauge mode, fused daily pooling) with the fast forward: daily series and
     L1 loss within tolerance of the exact kernel, parameter gradients norm-rel."""
     net = synthetic.forest(synthetic.loguniform_sizes(64, 100, 20000, 3), seed=13, single_inflow=0.25)
@@ -146,14 +155,14 @@ def test_fast_math_c3_daily_objective(cuda):
     obs = torch.from_numpy(np.random.default_rng(1).lognormal(0, 1, (len(outlets), w.D)).astype(np.float32)).to(cuda)
     g = RiverGraph(net.n, net.rows, net.cols, steps_hint=T)
     res = {}
-    for fast in (False, True):
+    for mode in ("exact", math):
         nt, qt, pt = (v.clone().requires_grad_(True) for v in (n, q, p))
-        daily, _, _, _ = route(g, qp, nt, qt, pt, length, slope, x, gauges=gz, daily=w, fast_math=fast)
+        daily, _, _, _ = route(g, qp, nt, qt, pt, length, slope, x, gauges=gz, daily=w, math=mode)
         loss = torch.nn.functional.l1_loss(daily[:, 3:], obs[:, 3:])
         loss.backward()
-        res[fast] = (daily.detach().cpu().numpy(), float(loss), nt.grad.cpu().numpy(), qt.grad.cpu().numpy(),
+        res[mode] = (daily.detach().cpu().numpy(), float(loss), nt.grad.cpu().numpy(), qt.grad.cpu().numpy(),
                      pt.grad.cpu().numpy())
-    f, e = res[True], res[False]
+    f, e = res[math], res["exact"]
     assert maxrel(f[0], e[0]) <= TOL
     assert abs(f[1] - e[1]) <= TOL * abs(e[1])
     for a, b in zip(f[2:], e[2:]):
