@@ -136,14 +136,21 @@ def cpu_baseline(args, net_global, x_const):
     grad = WORKLOADS[w]["grad"]
     t0 = time.perf_counter()
     res = O.route(no, r, qp, O.Bounds(), dtype=np.float32)
+    t_fwd = time.perf_counter() - t0
     if grad:
         W = np.random.default_rng(1).uniform(0, 1, (sample.n, T)).astype(np.float32)
         O.route_backward(no, r, qp, res["x"], W, O.Bounds())
     el = time.perf_counter() - t0
     what = ("fwd (fp32 + SciPy fp64 spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve)"
             if grad else "fwd (fp32 + SciPy fp64 spsolve_triangular per step)")
-    return {"value": sample.n * (T - 1) / el, "unit": "reach-timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s"}
+    rs = sample.n * (T - 1)
+    return {"value": rs / el, "unit": "reach-timesteps/s", "cores": 1, "kind": "port",
+            "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s",
+            "forward_only_value": rs / t_fwd,
+            # the reference itself (mmc.py + torch autograd, one core) measured in the build container on
+            # the same kind of trees: the port is a faster stand-in
+            "reference_measured": {"fwd_bwd": 1.3e5, "fwd_only": 3.0e6, "unit": "reach-timesteps/s",
+                                   "source": "BASELINE.md section 2 (2k-100k reaches, 8-core Xeon, 1 core)"}}
 
 
 def counter_file(args, lib_hash):
@@ -351,6 +358,9 @@ def main():
         if args.workload == "c5" and world == 1 and args.dropin_steps > 0:
             dropin = time_dropin(args, net, at, u, qprime, W, dev)
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, net, x_const)
+        if cpu is not None:
+            cpu["speedup_vs_port"] = value / cpu["value"]
+            cpu["speedup_vs_reference_measured"] = value / cpu["reference_measured"]["fwd_bwd" if spec["grad"] else "fwd_only"]
         largest = int(net.basin_sizes.max())
         out = {
             "metric": spec["metric"],

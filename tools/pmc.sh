@@ -16,7 +16,8 @@ run p1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_AC
 run p2 SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM &&
 run p3 FETCH_SIZE &&
 run p4 WRITE_SIZE TCC_HIT_sum TCC_MISS_sum &&
-run p5 GRBM_GUI_ACTIVE GRBM_COUNT TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
+run p5 GRBM_GUI_ACTIVE GRBM_COUNT TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum &&
+run p6 TCC_ATOMIC_sum TCC_EA0_WRREQ_STALL_sum TCC_TAG_STALL_sum TA_FLAT_ATOMIC_WAVEFRONTS_sum
 rc=$?
 python3 $R/tools/pmc_report.py $OUT > $OUT/report.txt 2>&1
 cat $OUT/report.txt

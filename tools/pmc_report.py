@@ -33,5 +33,10 @@ for k, d in sorted(vals.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0))
         fb = 2 * d.get("FETCH_SIZE", 0) * 1024
         wb = d.get("WRITE_SIZE", 0) * 1024
         print("   HBM-side bytes per dispatch: fetch %.4g (FETCH_SIZE x 2 KiB) + write %.4g = %.4g" % (fb, wb, fb + wb))
+    if "TCC_ATOMIC_sum" in d:
+        # RMW atomics reaching L2 (the backward's fp64 gradient flushes, the workgroup tickets; the
+        # cut-edge granules are plain agent-scope stores/loads) and write-path stall cycles
+        print("   L2 atomic requests per dispatch: %.4g; EA write-request stall cycles %.4g; tag stall %.4g" % (
+            d["TCC_ATOMIC_sum"], d.get("TCC_EA0_WRREQ_STALL_sum", 0), d.get("TCC_TAG_STALL_sum", 0)))
     for cn in sorted(d):
         print(f"   {cn:22s} {d[cn]:.4g}")
