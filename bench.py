@@ -235,7 +235,10 @@ def main():
     consts = RouteConsts()
     lib = _lib.load()
     lib_hash = lib.ddr_version().decode().split()[-1]
-    fwd_bytes, bwd_bytes = (8, 8) if args.workload == "c3" else (12, 12)  # SURVEY §8(d); gauge mode: no runoff
+    # algorithmic bytes per reach-step: forward q' read + x_save write + runoff write (gauge mode:
+    # no runoff); backward dL/drunoff read + x_save read -- the fp32 adjoint never reads q' (the c4 term of
+    # the VJP folds through the forward identity x = c1 Sx + c2 I + c3 Q + c4 qc, physics.h adjoint_step_fast)
+    fwd_bytes, bwd_bytes = (8, 8) if args.workload == "c3" else (12, 8)
 
     # ---- the step of each workload --------------------------------------------------------------------
     if args.workload == "c5":
