@@ -343,3 +343,61 @@ def test_1m_forest_two_generations(cuda):
         assert bool(torch.isfinite(ff.out[k]).all()), k
     del ff.qprime, ff.W, ff.out
     torch.cuda.empty_cache()
+
+
+# ---- C4: MERIT-shaped 350k reaches, water-year forward + 365-day geometry statistics --------------
+
+
+def test_c4_full_size_sampled_basins(cuda):
+    """BASELINE config 4 at full size: the 350k-reach MERIT-shaped forest (x = 0.3) routed forward over
+    8760 h (exact mode) and its 365-day geometry statistics in the fused pipeline.  Basins are
+    independent in both, so sampled basins (small ones and a basin split across workgroups) are checked
+    against the oracle routing / accumulating that basin alone."""
+    from ddr_amd.geometry.statistics import geometry_statistics_from_inflow
+
+    net = synthetic.forest(synthetic.zipf_sizes(350_000, 1000, 0.35), seed=4, single_inflow=0.15)
+    T = T_FULL
+    at = synthetic.reach_attributes(net.n, 4, x_const=0.3)
+    u = synthetic.unit_parameters(net.n, 4)
+    n, q, p = _physical(u)
+    slope = np.maximum(at.slope, np.float32(1e-3))
+    qp = synthetic.lateral_inflow_torch(net.n, T, seed=4, device=cuda)
+    g = RiverGraph(net.n, net.rows, net.cols)
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    with torch.no_grad():
+        runoff, _, _, _ = route(g, qp, tt(n), tt(q), tt(p), tt(at.length), tt(slope), tt(at.x),
+                                consts=RouteConsts(), math="exact")
+        q_daily = qp[::24][:365].contiguous()
+        stats = geometry_statistics_from_inflow(g, q_daily, tt(n), tt(p), tt(q), tt(slope))
+    torch.cuda.synchronize()
+    assert runoff.shape == (net.n, T) and bool(torch.isfinite(runoff).all())
+    ff = FullForest.__new__(FullForest)
+    ff.net, ff.T, ff.dev, ff.graph = net, T, cuda, g
+    members, nblk = _basins_by_blocks(ff)
+    sizes = np.array([len(m) for m in members])
+    rng = np.random.default_rng(3)
+    cand = np.flatnonzero((sizes >= 20) & (sizes <= 300))
+    pick = list(rng.choice(cand, size=3, replace=False))
+    multi = [i for i in range(len(members)) if nblk[i] >= 2]
+    assert multi
+    pick.append(min(multi, key=lambda i: len(members[i])))
+    for b in pick:
+        ids = np.sort(members[b])
+        keep = np.zeros(net.n, bool)
+        keep[ids] = True
+        ns, rs, cs, _ = extract_basins(net.n, net.rows, net.cols, keep)
+        onet = O.Network.from_coo(ns, rs, cs)
+        r = O.Reaches(n[ids], q[ids], p[ids], at.length[ids], slope[ids], at.x[ids])
+        sel = torch.from_numpy(ids).to(cuda)
+        qb = qp[:, sel].cpu().numpy()
+        ref = O.route(onet, r, qb, O.Bounds(), dtype=np.float32)
+        assert maxrel(runoff[sel].cpu().numpy(), ref["runoff"]) <= 1e-6, b
+        acc = O.accumulate_daily(onet, q_daily[:, sel].cpu().numpy())
+        orc = O.geometry_statistics(n[ids], p[ids], q[ids], slope[ids], acc)
+        for k, v in stats.items():
+            # means: the kernel sums the 365 days in fp64, the reference (numpy nanmean on fp32,
+            # statistics.py:20-83) pairwise in fp32 -- a few ulp apart at 365 terms; min/max/median exact
+            tol = 5e-6 if k.endswith("_mean") else 0.0
+            assert maxrel(v[ids], orc[k]) <= tol, (b, k)
+    del runoff, qp
+    torch.cuda.empty_cache()
