@@ -153,6 +153,8 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
   int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + target - 1) / target));
   const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
+  // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
+  const double fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
 
   // Splitting works on full-subtree sizes and heights: sub(i) = reaches draining through i,
   // ht(i) = longest path from i up to a source.
@@ -264,7 +266,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     for (size_t p = 0; p < pieces.size(); ++p) {
       const int64_t r = pieces[p].root;
       const double L = (double)(ht[r] + g->dist[r] + kChunk * (hops_down[p] + pieces[p].height));
-      fac[p] = weighted ? (steps + L) / steps : 1.0;
+      fac[p] = weighted ? std::pow((steps + L) / steps, fac_pow) : 1.0;
     }
     for (size_t p = 0; p < pieces.size(); ++p) wsum += (double)pieces[p].size * fac[p];
     // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
