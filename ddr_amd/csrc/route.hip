@@ -33,6 +33,11 @@
 
 namespace ddr {
 
+// experiments: the fp32 adjoint's recompute in the exact operation set (profiles/r02: no accuracy gain)
+#ifndef DDR_BWD_EXACT
+#define DDR_BWD_EXACT 0
+#endif
+
 namespace {
 
 constexpr unsigned long long kSentinel = ~0ull;
@@ -355,6 +360,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   unsigned up[KR];
   auto off_of = [&](int k) { return off[k] & 0xFFFF; };
   R Q[KR], In[KR], qa[KR], qb[KR], ex[KR], inv[KR];  // ex, inv: the static divisions, kept in registers
+  // one reach per thread (small blocks: light loads, where a tick is one dependency chain long): the
+  // statics stay in registers, off the chain's LDS round trips
+  constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
+  ReachStatic<R> sreg[kStatReg ? KR : 1];
   // runoff (N, T) written from here: the last four steps of each reach, stored 16 B at a time
   R ob0[KR], ob1[KR], ob2[KR], ob3[KR];
   R* runoff = static_cast<R*>(a.runoff);
@@ -377,6 +386,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     ex[k] = st.expo;
     inv[k] = st.inv_n;
     if (hk) tab.put(r, st);
+    if constexpr (kStatReg) sreg[k] = tab.get_pre(hk ? r : 0, st.expo, st.inv_n);  // the values the LDS path reads
   }
   if (tid == 0) sx[S - 1] = 0.0;
   const bool vown = tid < B.nvirt;
@@ -456,7 +466,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
         const int r = tq + (k0 + h) * BS;
-        st[h] = tab.get_pre(r < B.nloc ? r : 0, ex[k0 + h], inv[k0 + h]);
+        if constexpr (kStatReg) st[h] = sreg[k0 + h];
+        else st[h] = tab.get_pre(r < B.nloc ? r : 0, ex[k0 + h], inv[k0 + h]);
         Qv[h] = Q[k0 + h];
       }
       if (!accum) {
@@ -650,6 +661,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
   // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
   R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  // one reach per thread: the derived statics stay in registers (see the forward)
+  constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
+  ReachStatic<R> sreg[kStatReg ? KR : 1];
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -664,6 +678,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     pn[k] = pq[k] = pp[k] = R(0);
     g0[k] = g1[k] = g2[k] = g3[k] = R(0);
     if (hk) tab.put(r, load_static<R>(a, ref[k]));
+    if constexpr (kStatReg) {
+      const ReachStatic<R> ls = load_static<R>(a, ref[k]);
+      // the LDS path derives the same fields with the same operations each tick (StatTab::get)
+      sreg[k] = derive_static<R, !DDR_BWD_EXACT>(ls.n, ls.qe, ls.p, ls.sqrtS, ls.L, ls.X);
+    }
   }
   for (int c = 0; c < B.ncout; ++c) {
     const int loc = a.s.cout_loc[B.cout0 + c];
@@ -861,10 +880,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int e4 = t & 3;
       const R gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
       const R xtk = xc[k];
-#ifndef DDR_BWD_EXACT
-#define DDR_BWD_EXACT 0
-#endif
-      const ReachStatic<R> st = tab.template get<!DDR_BWD_EXACT>(rs);
+      const ReachStatic<R> st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(rs);
       const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
       const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
