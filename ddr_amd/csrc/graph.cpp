@@ -151,7 +151,11 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   if (opts && opts->max_block_reaches > 0) hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, opts->max_block_reaches);
   int64_t target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu) * kBlocksPerCU;
   resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
-  int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + target - 1) / target));
+  // Capacity floor: one wave-slice per SIMD (4 x 64 reaches).  A tick costs ~0.66 us + 0.49 us per
+  // slice on the busiest SIMD, so a light load (n well below 256 x 1024) is
+  // cheapest spread thin over many workgroups, not packed into a few full ones.
+  const int64_t min_cap = std::min<int64_t>(kMinBlockCap, bs);
+  int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(min_cap, (n + target - 1) / target));
   const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
   // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
   const double fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
@@ -382,7 +386,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       if (++gen > 64) return fail(DDR_ERR_CAPACITY, "graph cannot be packed into workgroups");
       weighted = true;
       const int64_t per_gen = std::min<int64_t>(target, resident) * gen;
-      cap = std::min<int64_t>(hard_cap, std::max<int64_t>(bs, (n + per_gen - 1) / per_gen));
+      cap = std::min<int64_t>(hard_cap, std::max<int64_t>(min_cap, (n + per_gen - 1) / per_gen));
       continue;
     }
     phase("lds");

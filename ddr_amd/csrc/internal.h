@@ -26,6 +26,11 @@ constexpr int kBlocksPerCU = 1024 / kBlockThreads;
 // Default workgroup capacity (reaches): KR = 4 reaches per thread.  The LDS check of the builder
 // lowers it when a block's slots and import rings would not fit.
 constexpr int kDefaultBlockReaches = kBlockThreads * kMaxKR;
+// Smallest workgroup capacity the packer aims for when the network is small (graph.cpp).
+#ifndef DDR_MIN_BLOCK_CAP
+#define DDR_MIN_BLOCK_CAP 256
+#endif
+constexpr int kMinBlockCap = DDR_MIN_BLOCK_CAP;
 // LDS budget per workgroup (160 KiB per CU).
 constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
 // Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").  Every

@@ -42,7 +42,7 @@ for N in Ns:
             q = uq * 1.0
             p = torch.exp(up * (np.log(200.0) - np.log(1.0 + 1e-6)) + np.log(1.0 + 1e-6))
             out, _, _, _ = route(g, qp, n, q, p, tt(at.length), tt(np.maximum(at.slope, np.float32(1e-3))), tt(at.x),
-                                 consts=RouteConsts(), fast_math=os.environ.get("DDR_FAST") == "1")
+                                 consts=RouteConsts(), math=os.environ.get("DDR_MATH", "faithful"))
             out.backward(W)
 
         step()
@@ -63,4 +63,5 @@ t1 = res[Ns[0]]["ms_max"] if Ns[0] == 1 else None
 for N in Ns:
     if t1:
         res[N]["speedup"] = round(t1 / res[N]["ms_max"], 2)
-print(json.dumps({"workload": wl, "T": T, "reaches": net.n, "predicted": res}))
+print(json.dumps({"workload": wl, "T": T, "reaches": net.n, "math": os.environ.get("DDR_MATH", "faithful"),
+                  "predicted": res}))
