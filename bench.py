@@ -548,6 +548,7 @@ def block_profile(path, g, step, lib):
         if len(ph):
             tot = ph.sum(0).astype(np.float64)
             out[key + "_phase_frac"] = (tot / tot.sum()).tolist()
+            out[key + "_phase_waves"] = ph.tolist()  # per wave (block-major, 16 waves), 8 phase counters
             log(f"[profile] {key} phases (cycle share over {len(ph)} waves): "
                 + " ".join(f"{f:.3f}" for f in tot / tot.sum()))
         t0 = p[:, 0].min()

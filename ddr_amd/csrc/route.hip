@@ -389,11 +389,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if constexpr (kStatReg) sreg[k] = tab.get_pre(hk ? r : 0, st.expo, st.inv_n);  // the values the LDS path reads
   }
   if (tid == 0) sx[S - 1] = 0.0;
-  const bool vown = tid < B.nvirt;
+#ifndef DDR_FWD_VOWN_HIGH
+#define DDR_FWD_VOWN_HIGH 1
+#endif
+  // virtual inflow vi is imported and published by thread BS - 1 - vi: the owners sit in the last
+  // waves, which hold fewer wave-slices than wave 0 when nloc is not a multiple of 1024 (the import's
+  // global round trip lands on the lighter waves; only the owner reads its ring entries, so the import
+  // needs no workgroup barrier)
+  const int vi = DDR_FWD_VOWN_HIGH ? BS - 1 - tid : tid;
+  const bool vown = vi < B.nvirt;
   int v_off = 0, v_edge = 0;
   if (vown) {
-    v_off = a.s.v_off[B.virt0 + tid];
-    v_edge = a.s.v_edge[B.virt0 + tid];
+    v_off = a.s.v_off[B.virt0 + vi];
+    v_edge = a.s.v_edge[B.virt0 + vi];
   }
   load_math_tables();
   load_xlist(a, B, xl);
@@ -444,10 +452,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           wait_granules<kImportBatch>(a.bnd + (int64_t)v_edge * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status, bid,
                                       force_to);
 #pragma unroll
-          for (int i = 0; i < kImportBatch; ++i) ring[tid * kChunk + h + i] = g[i];
+          for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunk + h + i] = g[i];
         }
       }
-      lds_barrier();
+#ifndef DDR_FWD_IMPORT_BARRIER
+#define DDR_FWD_IMPORT_BARRIER 0
+#endif
+      if (DDR_FWD_IMPORT_BARRIER) lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     phz.mark(1);  // import
@@ -565,7 +576,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     }
     if (vown) {
       const int t = tau - v_off;
-      if (t >= 0 && t < T) sx[B.nloc + tid] = ring[tid * kChunk + (tau % kChunk)];
+      if (t >= 0 && t < T) sx[B.nloc + vi] = ring[vi * kChunk + (tau % kChunk)];
     }
     phz.mark(4);  // publish
     lds_barrier();
