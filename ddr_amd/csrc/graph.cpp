@@ -159,6 +159,9 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
   // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
   const double fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
+  // block capacity rounded down to a multiple of this many reaches (a tick costs per 256-reach
+  // slice-per-SIMD unit; experiments: DDR_PACK_QUANT)
+  const int64_t pack_quant = getenv("DDR_PACK_QUANT") ? atol(getenv("DDR_PACK_QUANT")) : 1;
 
   // Splitting works on full-subtree sizes and heights: sub(i) = reaches draining through i,
   // ht(i) = longest path from i up to a source.
@@ -311,7 +314,10 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
         if (best < 0) {
           best = (int64_t)load.size();
           load.push_back(0);
-          bcap.push_back(std::min<double>((double)hard_cap, std::max<double>((double)sz, capw / fac[p])));
+          double bc = std::min<double>((double)hard_cap, std::max<double>((double)sz, capw / fac[p]));
+          if (pack_quant > 1 && bc >= (double)pack_quant)
+            bc = std::max<double>((double)sz, std::floor(bc / (double)pack_quant) * (double)pack_quant);
+          bcap.push_back(bc);
         }
         load[best] += sz;
         block_of_piece[p] = best;
