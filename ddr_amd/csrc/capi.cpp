@@ -1,5 +1,6 @@
 // C ABI of libddr_mc.so (include/ddr_mc.h).  No exception crosses this boundary; errors are
 // returned as ddr_status codes with a thread-local message (ddr_last_error).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -213,9 +214,20 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
 }
 
 template <typename R>
+ddr_status gauge_args(const ddr_graph* gh, const R* x_save, int64_t T, const ddr_gauges* gz, double qlb,
+                      int32_t flags, GaugeArgs& a);
+
+// Workspace of the state-gradient backward: dL/d(q' * flow_scale) in the schedule layout, then one
+// byte per gauge (the t = 0 clamp mask).
+int64_t state_work_bytes(const Graph* g, int64_t T, int64_t n_gauges, size_t rsize) {
+  return (int64_t)align16(rsize * (size_t)(g->n * T + g->sum_dn)) + n_gauges;
+}
+
+template <typename R>
 ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, const R* qprime,
                          int64_t T, const R* x_save, const double* bnd, const R* grad, const ddr_gauges* gauges,
-                         double* bwd_bnd, void* status, R* gn, R* gq, R* gp, int32_t flags, void* stream) {
+                         double* bwd_bnd, void* status, R* gn, R* gq, R* gp, int32_t flags, void* stream,
+                         int64_t qp_rows = 0, R* gqp = nullptr, R* gq0 = nullptr, void* work = nullptr) {
   ddr_status st = check_common<R>(gh, c, r, T);
   if (st) return st;
   const Graph* g = reinterpret_cast<const Graph*>(gh);
@@ -226,6 +238,13 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   if (flags & DDR_FWD_ACCUMULATE) return fail(DDR_ERR_ARG, "DDR_FWD_ACCUMULATE launches have no adjoint");
   if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
     return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
+  const bool state = gqp || gq0;
+  if (state) {
+    if (!work) return fail(DDR_ERR_ARG, "state gradients need the workspace (ddr_state_work_bytes)");
+    if (gq0 && !(flags & DDR_FWD_CARRY)) return fail(DDR_ERR_ARG, "grad_q0 needs a carried-state forward (DDR_FWD_CARRY)");
+    if (gqp && qp_rows < (T + std::max<int64_t>(1, r->qprime_hours) - 1) / std::max<int64_t>(1, r->qprime_hours))
+      return fail(DDR_ERR_ARG, "grad_qprime has fewer rows than the window reads");
+  }
   if ((st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, true))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -247,9 +266,22 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   a.gp = gp;
   // workspace: [2 n_cut T f64 boundary][3 N f64 accumulators]; the kernel reads grad (N, T) itself
   a.prof = g_prof[1];
+  if (state) {
+    a.gqs = work;
+    a.gq0 = gq0;
+    if (gauges && gauges->n_gauges > 0) {
+      // the gauge sums' clamp at t = 0 (mmc.py:398-412) gates dL/dout[:, 0]
+      GaugeArgs ga;
+      if ((st = gauge_args<R>(gh, x_save, T, gauges, c->discharge_lb, flags, ga))) return st;
+      unsigned char* mask = static_cast<unsigned char*>(work) + align16(sizeof(R) * (size_t)(g->n * T + g->sum_dn));
+      DDR_HIP(launch_gauge_mask0<R>(ga, x_save, mask, s));
+      a.gmask0 = mask;
+    }
+  }
   DDR_HIP(timing_mark(1, 0, s));
   DDR_HIP(launch_route<R>(g, a, true, s));
   DDR_HIP(timing_mark(1, 1, s));
+  if (gqp) DDR_HIP(launch_scatter_qprime_grad<R>(g, a, qp_rows, gqp, s));
   return g_pending.enqueue(status, s, "backward");
 }
 
@@ -425,6 +457,24 @@ ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const
                                const double* grad, const ddr_gauges* gauges, double* bwd_bnd, void* status,
                                double* gn, double* gq, double* gp, int32_t flags, void* stream) {
   DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream); })
+}
+int64_t ddr_state_work_bytes(const ddr_graph* g, int64_t T, int64_t n_gauges, int32_t real_bytes) {
+  if (!g || T < 1 || n_gauges < 0 || (real_bytes != 4 && real_bytes != 8)) return -1;
+  return state_work_bytes(reinterpret_cast<const Graph*>(g), T, n_gauges, (size_t)real_bytes);
+}
+ddr_status ddr_mc_backward_state_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                     const float* qprime, int64_t qprime_rows, int64_t T, const float* x_save,
+                                     const double* bnd, const float* grad, const ddr_gauges* gauges, double* bwd_bnd,
+                                     void* status, float* gn, float* gq, float* gp, float* grad_qprime,
+                                     float* grad_q0, void* work, int32_t flags, void* stream) {
+  DDR_GUARD({ return backward_impl<float>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work); })
+}
+ddr_status ddr_mc_backward_state_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                     const double* qprime, int64_t qprime_rows, int64_t T, const double* x_save,
+                                     const double* bnd, const double* grad, const ddr_gauges* gauges, double* bwd_bnd,
+                                     void* status, double* gn, double* gq, double* gp, double* grad_qprime,
+                                     double* grad_q0, void* work, int32_t flags, void* stream) {
+  DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work); })
 }
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T, const ddr_gauges* gz,
                                 double qlb, int32_t flags, float* out, void* stream) {

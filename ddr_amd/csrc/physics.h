@@ -393,7 +393,7 @@ __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, c
 // ~90 other instructions.  Uses x(t) = c1 Sx + c2 I + c3 Q + c4 qc (the forward solve) to collapse
 // sum_k gc_k c_k into gb x.
 struct AdjOut {
-  float c1, c2, c3, gQ, gn, gq, gp;
+  float c1, c2, c3, c4, gQ, gn, gq, gp;
 };
 __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s, float Q, const Consts<float>& c,
                                                     float gb, float x, float Sx, float I) {
@@ -436,6 +436,7 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
   o.c2 = (c.dt + tX) * rden;
   const float c4 = (2.0f * c.dt) * rden;
   o.c3 = 1.0f - c4;
+  o.c4 = c4;
   // ---- VJP: gc = gb (Sx, I, Q, qc); sum_k gc_k c_k = gb x ----
   const float g_twok = gb * fmaf(s.X, I - Sx, omX * (Q - x)) * rden;
   const float g_cel = -(g_twok * twok) * rcel;                    // k = L / cel

@@ -632,7 +632,10 @@ __device__ __forceinline__ Grad4<R> make_grad4(R a, R b, R c, R d) { return Grad
 // states x(t - 3) (the schedule layout, coalesced rows), the virtual inflows' x, and dL/drunoff read
 // straight from the API's (N, T) layout in 16-B groups of four steps (gauge mode: summed over the
 // reach's gauges from (G, T)).
-template <typename R, int KR>
+// GS (state gradients, DDR_BWD_GRAD_*): the sweep also runs step 0 -- the hot start's transposed solve
+// (c1 = 1) into dL/d(q' * flow_scale)[0], or dL/dQ0 of a carried state -- and writes dL/d(q' * flow_scale)
+// of every step (gb c4 [q' >= q_lb], mmc.py:421-424, 535-538) into gqs, the schedule layout of qs.
+template <typename R, int KR, bool GS>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -658,6 +661,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
   const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
+  const int tmin = GS ? 0 : 1;                  // first step of the sweep (step 0: the hot start / Q0)
+  R* gqs = static_cast<R*>(a.gqs);
+  const R* qsp = static_cast<const R*>(a.qs);
 
   // od packs the tick offset (bits 16-30), dl (low 16, signed): local downstream (>= 0),
   // -(import slot + 2), or -1, and bit 31: the reach has no dL/drunoff row (gauge mode, ungauged
@@ -672,6 +678,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
   // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
   R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  R qsv[GS ? KR : 1];  // state gradients: q' * flow_scale of this tick's step (prefetched a tick ahead)
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
   ReachStatic<R> sreg[kStatReg ? KR : 1];
@@ -746,23 +753,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
     const int64_t i1 = base + 1 < T ? base + 1 : T - 1, i2 = base + 2 < T ? base + 2 : T - 1,
                   i3 = base + 3 < T ? base + 3 : T - 1;
-    auto add_row = [&](const R* row) {
+    // m0: the gauge's t = 0 sum passed its clamp (state gradients only; mmc.py:398-412)
+    auto add_row = [&](const R* row, bool m0) {
       if (vec4) {
         if constexpr (sizeof(R) == 4) {
           const float4 v = *reinterpret_cast<const float4*>(row + base);
-          v0 = v0 + v.x; v1 = v1 + v.y; v2 = v2 + v.z; v3 = v3 + v.w;
+          v0 = v0 + (m0 ? v.x : 0.0f); v1 = v1 + v.y; v2 = v2 + v.z; v3 = v3 + v.w;
         } else {
           const double2 u = reinterpret_cast<const double2*>(row + base)[0];
           const double2 w = reinterpret_cast<const double2*>(row + base)[1];
-          v0 = v0 + u.x; v1 = v1 + u.y; v2 = v2 + w.x; v3 = v3 + w.y;
+          v0 = v0 + (m0 ? u.x : 0.0); v1 = v1 + u.y; v2 = v2 + w.x; v3 = v3 + w.y;
         }
       } else {
-        v0 = v0 + row[base]; v1 = v1 + row[i1]; v2 = v2 + row[i2]; v3 = v3 + row[i3];
+        v0 = v0 + (m0 ? row[base] : R(0)); v1 = v1 + row[i1]; v2 = v2 + row[i2]; v3 = v3 + row[i3];
       }
     };
     if (a.g_roff) {
       const int64_t q1 = a.g_roff[ref + 1];
-      for (int64_t q = a.g_roff[ref]; q < q1; ++q) add_row(gout + a.g_rg[q] * T);
+      for (int64_t q = a.g_roff[ref]; q < q1; ++q) {
+        const int64_t gi = a.g_rg[q];
+        add_row(gout + gi * T, !(GS && base == 0 && a.gmask0 && a.gmask0[gi] == 0));
+      }
       return make_grad4(v0, v1, v2, v3);
     }
     // one reach row: the loaded values as they are (adding them to 0 would consume the load now)
@@ -808,7 +819,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int c = w / kChunk, sidx = w % kChunk;
         const int t = (tau - sidx) - (int)(own[c] >> 16);
         R A = R(0), Bv = R(0);
-        if (t >= 1 && t < T) {
+        if (t >= tmin && t < T) {
           double g[2];
           wait_granules<2>(a.bwd_bnd + ((int64_t)(B.cout0 + c) * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
           A = R(g[0]);
@@ -827,7 +838,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // step tau + 1 - off_c = tau - v_off) to the upstream block; publish the upstream reach's x
       // at the consumer's current step - 1
       const int t = tau - v_off;
-      if (t >= 1 && t < T) {
+      if (t >= tmin && t < T) {
         const int dloc = v_dloc_of();
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
@@ -897,13 +908,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
       const R gb = R(gb64);
       const R Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);     // Q_{t-1}
-      R c1, c2, c3, gQ, gn, gq, gp;
+      R c1, c2, c3, c4, gQ, gn, gq, gp;
       if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
         const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
-        c1 = o.c1; c2 = o.c2; c3 = o.c3; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
+        c1 = o.c1; c2 = o.c2; c3 = o.c3; c4 = o.c4; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
       } else {
         const R qvk = static_cast<const R*>(a.qs)[xs_base + (int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale
-        R c4, tw, ss;
+        R tw, ss;
         Geom<R> geo;
         coefficients<R, !DDR_BWD_EXACT>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
         const R qc = rmax(qvk, cs.qlb);
@@ -927,6 +938,26 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         sa[r] = R((double)c1 * gb64);
         sb[r] = c2 * gb;
         lam[k] = ((gb * c3) + gQ) + Bd[k];
+        // dL/dqc = gb c4 (b = ... + c4 qc), through qc = clamp(q' * flow_scale) (mmc.py:421-424)
+        if constexpr (GS) gqs[xs_base + (int64_t)tau * B.nloc + r] = (qsv[k] >= cs.qlb) ? gb * c4 : R(0);
+      } else if (GS && hk && t == 0) {
+        if (carry) {
+          // Q0 = q0 feeds step 1 unclamped; runoff[:, 0] = clamp(q0) per reach, or the gauge sum's clamp
+          // (already folded into gk through gmask0)
+          if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = a.g_roff ? lm : lam[k] + ((xtk >= cs.qlb) ? gk : R(0));
+          gqs[xs_base + (int64_t)tau * B.nloc + r] = R(0);
+          sa[r] = R(0);
+          sb[r] = R(0);
+        } else {
+          // hot start x(0) = (I - N)^-1 q'[0] (mmc.py:25-66): its transposed solve (c1 = 1) is gb64
+          gqs[xs_base + (int64_t)tau * B.nloc + r] = gb;
+          sa[r] = gb;
+          sb[r] = R(0);
+        }
+      }
+      if constexpr (GS) {
+        const int tn = tau > 0 ? tau - 1 : 0;  // the next backward tick's row
+        qsv[k] = qsp[xs_base + (int64_t)tn * B.nloc + rs];
       }
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
@@ -950,6 +981,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2, x(t-2) at row TT-3
+  if constexpr (GS) {
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int r = tid + k * BS;
+      qsv[k] = qsp[xs_base + (int64_t)(TT - 1) * B.nloc + (r < B.nloc ? r : 0)];
+    }
+  }
   load_own(TT - 1, xc, tid);
   load_own(TT - 2, xa, tid);
   load_own(TT - 3, xb, tid);
@@ -1067,6 +1105,32 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   }
 }
 
+// Adjoint of gather_qprime: dL/dq'[s, ref] = flow_scale[ref] * sum over the steps t reading row s
+// (ascending t) of gqs[tick(t, ref)]; 0 for a divide filled with 0.001 (readers.py:523-530).  Step t
+// reads row max(t - 1, 0) / qp_hours (mmc.py:421-424 for t >= 1, the hot start for t = 0).  One
+// thread per (row, reference reach): the writes are coalesced rows of q'.
+template <typename R>
+__global__ void scatter_qprime_grad_kernel(RouteArgs a, int64_t rows, R* out) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t N = a.N, T = a.T, H = a.qp_hours;
+  if (w >= rows * N) return;
+  const int64_t srow = w / N;
+  const int ref = (int)(w % N);
+  const int P = a.s.pos_of_ref[ref];
+  const BlockDesc B = a.s.blocks[a.s.block_of_pos[P]];
+  const int64_t r = P - B.pos0, o = a.s.off[P];
+  const R* g = static_cast<const R*>(a.gqs) + T * B.pos0 + B.pre_dn;
+  // steps whose row is srow: max(t - 1, 0) in [srow H, srow H + H)
+  int64_t t0 = srow * H + 1, t1 = srow * H + H + 1;
+  if (srow == 0) t0 = 0;
+  t1 = t1 < T ? t1 : T;
+  R acc = R(0);
+  for (int64_t t = t0; t < t1; ++t) acc = acc + g[(t + o) * B.nloc + r];
+  if (a.qp_valid && !a.qp_valid[ref]) acc = R(0);
+  if (a.fs) acc = acc * static_cast<const R*>(a.fs)[ref];
+  out[w] = acc;
+}
+
 // ============================================================================================
 // Gauge reduction: out[g, t] = sum_{k} clamp(x_t[idx_k])  (mmc.py:405-411, 433-439)
 // ============================================================================================
@@ -1087,6 +1151,22 @@ __global__ void gauge_reduce_kernel(GaugeArgs a, const R* xsave, R* out) {
   }
   // output[:, 0] = clamp(initial) (mmc.py:412); later steps are sums of clamped states
   out[g * a.T + t] = (t == 0) ? rmax_nan(acc, R(a.qlb)) : acc;
+}
+
+// mask[g] = 1 where the t = 0 gauge sum (before its clamp, as gauge_reduce_kernel) is >= q_lb:
+// torch.clamp's backward passes the gradient there (inclusive at the bound).
+template <typename R>
+__global__ void gauge_mask0_kernel(GaugeArgs a, const R* xsave, unsigned char* mask) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.G) return;
+  R acc = R(0);
+  for (int64_t k = a.goff[g]; k < a.goff[g + 1]; ++k) {
+    const int P = a.pos_of_ref[a.gidx[k]];
+    const BlockDesc B = a.s.blocks[a.block_of_pos[P]];
+    const R x = xsave[a.T * B.pos0 + B.pre_dn + (int64_t)a.s.off[P] * B.nloc + (P - B.pos0)];
+    acc = acc + (a.carry ? x : rmax_nan(x, R(a.qlb)));
+  }
+  mask[g] = (acc >= R(a.qlb)) ? 1 : 0;
 }
 
 // ============================================================================================
@@ -1161,7 +1241,7 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   a.own_off = a.xl_off - (int32_t)align16(4 * (size_t)std::max(g->max_virt, g->max_cout));
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
-    auto kern = route_backward_kernel<R, KR>;
+    auto kern = a.gqs ? route_backward_kernel<R, KR, true> : route_backward_kernel<R, KR, false>;
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
@@ -1198,9 +1278,9 @@ int max_resident_blocks(const Graph* g, bool backward) {
   const size_t smem = route_smem_bytes<R>(g, backward);
   const void* f = nullptr;
   switch (g->kr) {
-    case 1: f = backward ? (const void*)route_backward_kernel<R, 1> : (const void*)route_forward_kernel<R, 1, 0>; break;
-    case 2: f = backward ? (const void*)route_backward_kernel<R, 2> : (const void*)route_forward_kernel<R, 2, 0>; break;
-    default: f = backward ? (const void*)route_backward_kernel<R, 4> : (const void*)route_forward_kernel<R, 4, 0>;
+    case 1: f = backward ? (const void*)route_backward_kernel<R, 1, false> : (const void*)route_forward_kernel<R, 1, 0>; break;
+    case 2: f = backward ? (const void*)route_backward_kernel<R, 2, false> : (const void*)route_forward_kernel<R, 2, 0>; break;
+    default: f = backward ? (const void*)route_backward_kernel<R, 4, false> : (const void*)route_forward_kernel<R, 4, 0>;
   }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;
@@ -1221,6 +1301,22 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + G - 1) / G));
   hipLaunchKernelGGL(kern, grid, dim3(1024), smem, stream, a);
+  return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_scatter_qprime_grad(const Graph* g, const RouteArgs& a, int64_t rows, R* out, hipStream_t stream) {
+  const int64_t total = rows * g->n;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(scatter_qprime_grad_kernel<R>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, a,
+                     rows, out);
+  return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_gauge_mask0(const GaugeArgs& a, const R* xsave, unsigned char* mask, hipStream_t stream) {
+  if (a.G == 0) return hipSuccess;
+  hipLaunchKernelGGL(gauge_mask0_kernel<R>, dim3((unsigned)((a.G + 255) / 256)), dim3(256), 0, stream, a, xsave, mask);
   return hipGetLastError();
 }
 
@@ -1260,6 +1356,10 @@ template int max_resident_blocks<float>(const Graph*, bool);
 template int max_resident_blocks<double>(const Graph*, bool);
 template hipError_t launch_gather_qprime<float>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_gather_qprime<double>(const Graph*, RouteArgs&, hipStream_t);
+template hipError_t launch_scatter_qprime_grad<float>(const Graph*, const RouteArgs&, int64_t, float*, hipStream_t);
+template hipError_t launch_scatter_qprime_grad<double>(const Graph*, const RouteArgs&, int64_t, double*, hipStream_t);
+template hipError_t launch_gauge_mask0<float>(const GaugeArgs&, const float*, unsigned char*, hipStream_t);
+template hipError_t launch_gauge_mask0<double>(const GaugeArgs&, const double*, unsigned char*, hipStream_t);
 template hipError_t launch_gauge<float>(const GaugeArgs&, const float*, float*, hipStream_t);
 template hipError_t launch_gauge<double>(const GaugeArgs&, const double*, double*, hipStream_t);
 

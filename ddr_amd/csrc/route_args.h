@@ -43,6 +43,11 @@ struct RouteArgs {
   void* gn;
   void* gq;
   void* gp;
+  // state-gradient backward (route_backward_kernel<.., GS = true>): dL/d(q' * flow_scale) in the
+  // schedule layout (as qs), dL/dQ0 (N, carried state), per-gauge t = 0 clamp mask (gauge mode)
+  void* gqs;
+  void* gq0;
+  const unsigned char* gmask0;
   unsigned long long* prof;  // debug per-workgroup profile (ddr_set_block_profile), or null
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
   float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
@@ -63,6 +68,13 @@ struct GaugeArgs {
 
 template <typename R>
 hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipStream_t stream);
+// dL/dq' (rows of the caller's store, (rows, N)) from the state-gradient backward's gqs: the adjoint
+// of gather_qprime (sum over the steps reading each row, times flow_scale, 0 for a filled divide)
+template <typename R>
+hipError_t launch_scatter_qprime_grad(const Graph* g, const RouteArgs& a, int64_t rows, R* out, hipStream_t stream);
+// per-gauge clamp mask of the t = 0 gauge sum (mmc.py:398-412), for the state-gradient backward
+template <typename R>
+hipError_t launch_gauge_mask0(const GaugeArgs& a, const R* xsave, unsigned char* mask, hipStream_t stream);
 template <typename R>
 int max_resident_blocks(const Graph* g, bool backward);
 template <typename R>

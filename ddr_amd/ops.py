@@ -185,10 +185,13 @@ def _(qprime, n, q, p, length, slope, x_storage, flow_scale, q0, g_off, g_idx, r
 def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.Tensor, q: torch.Tensor,
                       p: torch.Tensor, length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor,
                       flow_scale: torch.Tensor | None, x_save: torch.Tensor, bnd: torch.Tensor,
-                      r_off: torch.Tensor | None, r_g: torch.Tensor | None, graph_id: int, consts: list[float],
-                      flags: int, steps: int, daily: list[int]) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial).  With ``daily`` the incoming gradient
-    is dL/d(daily series) (G, D): its pooling adjoint seeds the gauge-mode routing adjoint."""
+                      g_off: torch.Tensor | None, g_idx: torch.Tensor | None, r_off: torch.Tensor | None,
+                      r_g: torch.Tensor | None, qp_valid: torch.Tensor | None, graph_id: int, consts: list[float],
+                      flags: int, steps: int, qp_hours: int, daily: list[int], want_qprime: bool, want_q0: bool
+                      ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial), dL/dq' (shape of ``qprime``, or empty)
+    and dL/dQ0 (N, carried state, or empty).  With ``daily`` the incoming gradient is dL/d(daily
+    series) (G, D): its pooling adjoint seeds the gauge-mode routing adjoint."""
     g = _graph(graph_id)
     T, N = int(steps), qprime.shape[1]
     dev, dt = qprime.device, qprime.dtype
@@ -212,26 +215,44 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
     gp = torch.empty(N, device=dev, dtype=dt)
     bwd_bnd = torch.empty(g.bwd_numel(T), device=dev, dtype=torch.float64)
     status = torch.empty(g.info.status_bytes, device=dev, dtype=torch.uint8)
-    bwd = lib.ddr_mc_backward_f32 if f32 else lib.ddr_mc_backward_f64
-    r = _reaches(n, q, p, length, slope, x_storage, flow_scale)
+    r = _reaches(n, q, p, length, slope, x_storage, flow_scale, qp_hours, qp_valid)
     c = _consts(consts)
     gz = None
     if r_off is not None:
-        gz = _lib.Gauges(grad_runoff.shape[0], None, None, r_off.data_ptr(), r_g.data_ptr())
-    _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, x_save.data_ptr(),
-                   bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
-                   C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(),
-                   status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), int(flags), stream))
+        gz = _lib.Gauges(grad_runoff.shape[0], g_off.data_ptr() if g_off is not None else None,
+                         g_idx.data_ptr() if g_idx is not None else None, r_off.data_ptr(), r_g.data_ptr())
+    want_q0 = want_q0 and bool(flags & _lib.DDR_FWD_CARRY)
+    gqp = torch.empty(qprime.shape if want_qprime else (0,), device=dev, dtype=dt)
+    gq0 = torch.empty(N if want_q0 else 0, device=dev, dtype=dt)
+    if want_qprime or want_q0:
+        # state-gradient adjoint (route_backward_kernel<GS>): also the step-0 sweep and dL/dq'
+        G = grad_runoff.shape[0] if gz is not None else 0
+        work = torch.empty(int(lib.ddr_state_work_bytes(g.handle, T, G, 4 if f32 else 8)), device=dev,
+                           dtype=torch.uint8)
+        bwd = lib.ddr_mc_backward_state_f32 if f32 else lib.ddr_mc_backward_state_f64
+        _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), int(qprime.shape[0]), T, x_save.data_ptr(),
+                       bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
+                       C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(), status.data_ptr(),
+                       gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), gqp.data_ptr() if want_qprime else None,
+                       gq0.data_ptr() if want_q0 else None, work.data_ptr(), int(flags), stream))
+    else:
+        bwd = lib.ddr_mc_backward_f32 if f32 else lib.ddr_mc_backward_f64
+        _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, x_save.data_ptr(),
+                       bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
+                       C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(),
+                       status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), int(flags), stream))
     if _CHECK_STATUS:
         _lib.check(lib.ddr_status_check(1))
-    return gn, gq, gp
+    return gn, gq, gp, gqp, gq0
 
 
 @mc_route_backward.register_fake
-def _(grad_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g, graph_id, consts,
-      flags, steps, daily):
+def _(grad_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, g_off, g_idx, r_off, r_g,
+      qp_valid, graph_id, consts, flags, steps, qp_hours, daily, want_qprime, want_q0):
     N = qprime.shape[1]
-    return qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N)
+    want_q0 = want_q0 and bool(flags & _lib.DDR_FWD_CARRY)
+    return (qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N),
+            qprime.new_empty(qprime.shape if want_qprime else (0,)), qprime.new_empty(N if want_q0 else 0))
 
 
 def _setup_context(ctx, inputs, output):
@@ -249,12 +270,15 @@ def _setup_context(ctx, inputs, output):
     ctx.gauge = g_off is not None
     ctx.p_scalar = p.numel() == 1
     ctx.p_shape = p.shape
-    ctx.save_for_backward(qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g)
+    ctx.qp_hours = qp_hours
+    ctx.save_for_backward(qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, g_off, g_idx, r_off, r_g,
+                          qp_valid)
     ctx.set_materialize_grads(False)
 
 
 def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
-    qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, r_off, r_g = ctx.saved_tensors
+    (qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, g_off, g_idx, r_off, r_g,
+     qp_valid) = ctx.saved_tensors
     if g_tw is not None or g_ss is not None:
         if (g_tw is not None and bool(g_tw.ne(0).any())) or (g_ss is not None and bool(g_ss.ne(0).any())):
             raise NotImplementedError("gradients through top_width/side_slope are not supported by ddrx::mc_route")
@@ -271,11 +295,16 @@ def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
             # runoff[:, T-1] is the final state Q_{T-1}
             g_runoff = g_runoff.clone()
             g_runoff[:, T - 1] += g_qlast
-    gn, gq, gp = mc_route_backward(g_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd,
-                                   r_off, r_g, ctx.graph_id, ctx.consts, ctx.flags, T, ctx.daily)
+    # dL/dq' and dL/dQ0 (the carried state) when the caller's graph asks for them: route_timestep is
+    # differentiable w.r.t. both in the reference (mmc.py:487-559), the hot start w.r.t. q'[0]
+    want_qp = bool(ctx.needs_input_grad[0])
+    want_q0 = bool(ctx.needs_input_grad[8])
+    gn, gq, gp, gqp, gq0 = mc_route_backward(g_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save,
+                                             bnd, g_off, g_idx, r_off, r_g, qp_valid, ctx.graph_id, ctx.consts,
+                                             ctx.flags, T, ctx.qp_hours, ctx.daily, want_qp, want_q0)
     if ctx.p_scalar:
         gp = gp.sum().reshape(ctx.p_shape)
-    return (None, gn, gq, gp) + (None,) * 16
+    return ((gqp if want_qp else None), gn, gq, gp) + (None,) * 4 + ((gq0 if want_q0 else None),) + (None,) * 11
 
 
 mc_route.register_autograd(_backward, setup_context=_setup_context)
@@ -371,7 +400,8 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
     if steps is None:
         steps = qprime.shape[0] * max(1, qprime_hours)
     if save is None:
-        save = (not accumulate) and torch.is_grad_enabled() and any(t.requires_grad for t in (n, q, p))
+        save = (not accumulate) and torch.is_grad_enabled() and any(
+            t is not None and t.requires_grad for t in (n, q, p, qprime, q0))
     math = math or ("fast" if fast_math else "exact")
     if math not in ("exact", "faithful", "fast"):
         raise ValueError(f"math must be 'exact', 'faithful' or 'fast', not {math!r}")

@@ -66,9 +66,9 @@ def compute_hotstart_discharge(q_prime_t0: torch.Tensor, mapper: PatternMapper, 
         dev = q_prime_t0.device
         n = q_prime_t0.shape[0]
         one = torch.ones(n, device=dev, dtype=q_prime_t0.dtype)
-        with torch.no_grad():
-            _, q_last, _, _ = route(g, q_prime_t0.reshape(1, n), one, one, one, one, one, one,
-                                    consts=RouteConsts(discharge_lb=lb), save=False)
+        # differentiable w.r.t. q'[0] like the reference's solve (the adjoint's step-0 sweep)
+        _, q_last, _, _ = route(g, q_prime_t0.reshape(1, n), one, one, one, one, one, one,
+                                consts=RouteConsts(discharge_lb=lb))
         return q_last
     num_segments = q_prime_t0.shape[0]
     neg_ones = -torch.ones(num_segments, device=q_prime_t0.device)

@@ -213,6 +213,29 @@ ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const
                                double* bwd_bnd, void* status, double* grad_n, double* grad_q,
                                double* grad_p, int32_t flags, void* stream);
 
+/* State-gradient adjoint: ddr_mc_backward plus the gradients the reference's autograd delivers to
+ * the lateral inflow and the discharge state (routing/mmc.py:487-559 route_timestep is
+ * differentiable w.r.t. q_prime_clamp and _discharge_t; the hot start mmc.py:25-66 w.r.t. q'[0]):
+ *   grad_qprime (qprime_rows, N) dL/dq' in the caller's store layout (rows of qprime_hours steps;
+ *               flow_scale applied, 0 for a divide filled by qprime_valid), or NULL
+ *   grad_q0     (N) dL/dQ0 of a carried state (forward run with DDR_FWD_CARRY), or NULL
+ *   work        device workspace of ddr_state_work_bytes(g, T, n_gauges, sizeof(real)) bytes
+ * Replaces: torch autograd through mmc.py:421-424 (q' clamp), 535-538 (c4 q'), 25-66 (hot start)
+ * and the carried _discharge_t (mmc.py:330-342). */
+int64_t ddr_state_work_bytes(const ddr_graph* g, int64_t T, int64_t n_gauges, int32_t real_bytes);
+ddr_status ddr_mc_backward_state_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                     const float* qprime, int64_t qprime_rows, int64_t T, const float* x_save,
+                                     const double* bnd, const float* grad_runoff, const ddr_gauges* gauges,
+                                     double* bwd_bnd, void* status, float* grad_n, float* grad_q,
+                                     float* grad_p, float* grad_qprime, float* grad_q0, void* work,
+                                     int32_t flags, void* stream);
+ddr_status ddr_mc_backward_state_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                     const double* qprime, int64_t qprime_rows, int64_t T, const double* x_save,
+                                     const double* bnd, const double* grad_runoff, const ddr_gauges* gauges,
+                                     double* bwd_bnd, void* status, double* grad_n, double* grad_q,
+                                     double* grad_p, double* grad_qprime, double* grad_q0, void* work,
+                                     int32_t flags, void* stream);
+
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,

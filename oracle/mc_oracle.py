@@ -335,7 +335,8 @@ def route(net: Network, r: Reaches, qprime: np.ndarray, bd: Bounds = Bounds(), d
           q0: np.ndarray | None = None, dtype=np.float32, outflow_idx=None):
     """``MuskingumCunge.forward`` (mmc.py:365-443) with ``route_timestep`` (487-559).
 
-    Returns dict(runoff (N,T) or (G,T), x (T,N) unclamped solve result (x[0] = Q0),
+    Returns dict(runoff (N,T) or (G,T), x (T,N) unclamped solve result (x[0]: the hot start's
+    unclamped solve, or the carried Q0),
     q_last, top_width, side_slope).
     """
     f = dtype
@@ -343,12 +344,14 @@ def route(net: Network, r: Reaches, qprime: np.ndarray, bd: Bounds = Bounds(), d
     qprime = np.asarray(qprime, dtype=f)
     T, N = qprime.shape
     qlb = f(bd.discharge)
+    xs = np.zeros((T, N), dtype=f)
     if q0 is None:
-        Q = hotstart(net, qprime[0], bd, f)
+        # the hot start's unclamped solve (its clamp's backward masks where it is below q_lb)
+        xs[0] = net.lower_solve(np.ones(N), np.asarray(qprime[0], dtype=f)).astype(f)
+        Q = np.maximum(xs[0], qlb)
     else:
         Q = np.asarray(q0, dtype=f).copy()
-    xs = np.zeros((T, N), dtype=f)
-    xs[0] = Q
+        xs[0] = Q
     tw = ss = np.zeros(0, dtype=f)
     for t in range(1, T):
         qc = np.maximum(qprime[t - 1], qlb)
@@ -521,12 +524,15 @@ def _celerity_vjp(Q, n, q, p, slope, bd: Bounds, g_c):
 
 
 def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray, grad_runoff: np.ndarray,
-                   bd: Bounds = Bounds(), dt=3600.0, outflow_idx=None, want_qprime=False):
-    """Adjoint of ``route`` w.r.t. (n, q_spatial, p_spatial) (and optionally q'), fp64.
+                   bd: Bounds = Bounds(), dt=3600.0, outflow_idx=None, want_qprime=False, carry=False):
+    """Adjoint of ``route`` w.r.t. (n, q_spatial, p_spatial) (and optionally q' and the state), fp64.
 
     ``xs`` is the (T, N) unclamped solve output of the forward (``xs[0]`` = Q0).
     ``grad_runoff`` is dL/d runoff, (N, T) or (G, T) in gauge mode.
-    The hot start has no parameter dependence (mmc.py:337-342) so the sweep stops at t = 1.
+    The hot start has no parameter dependence (mmc.py:337-342) so the parameter sweep stops at t = 1;
+    with ``want_qprime`` step 0 adds the hot start's transposed solve (mmc.py:25-66) to dL/dq'[0].
+    ``carry``: the forward carried Q0 = ``xs[0]`` (``route(q0=...)``), which step 1 uses unclamped
+    (mmc.py:330-342, 487-559); ``q0`` of the result is then dL/dQ0.
     """
     f = np.float64
     r = r.astype(f)
@@ -535,15 +541,20 @@ def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray,
     T, N = xs.shape
     qlb = bd.discharge
     G = np.asarray(grad_runoff, dtype=f)
-    if outflow_idx is not None and len(outflow_idx) != N:
+    gauge = outflow_idx is not None and len(outflow_idx) != N
+    Qall = np.maximum(xs, qlb)
+    Q0 = xs[0] if carry else Qall[0]  # the state step 1 reads
+    if gauge:
         g_all = np.zeros((T, N))
         for g, idx in enumerate(outflow_idx):
             idx = np.asarray(idx, dtype=np.int64) % N
+            # output[:, 0] = clamp(sum of the gauge's initial states) (mmc.py:398-412)
+            m0 = float(np.sum(Q0[idx], dtype=np.float64) >= qlb)
             for j in idx:
                 g_all[:, j] += G[g]
+                g_all[0, j] += G[g, 0] * (m0 - 1.0)
     else:
         g_all = G.T
-    Qall = np.maximum(xs, qlb)
     lam = np.zeros(N)
     gn = np.zeros(N)
     gq = np.zeros(N)
@@ -554,6 +565,8 @@ def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray,
         lam = lam + g_all[t]
         gx = lam * (xs[t] >= qlb)
         Qp = Qall[t - 1]
+        if t == 1:
+            Qp = Q0
         c, _, _ = trapezoid_celerity(Qp, r.n, r.q, p_full, r.slope, bd, f)
         c1, c2, c3, c4 = muskingum_coefficients(r.length, c, r.x, dt, f)
         gb = net.upper_solve(c1, gx)
@@ -583,13 +596,17 @@ def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray,
         if want_qprime:
             gqp[t - 1] += gb * c4 * (qprime[t - 1] >= qlb)
         lam = up_push + gb * c3 + gQc
+    g0 = None
+    if carry:
+        # runoff[:, 0] = clamp(Q0) per reach (the gauge sums' clamp is already in g_all[0])
+        g0 = lam + g_all[0] * (1.0 if gauge else (xs[0] >= qlb))
     lam = lam + g_all[0]
-    if want_qprime:
+    if want_qprime and not carry:
         # hot start: Q0 = clamp(solve(I - N, q'[0]))
         gx0 = lam * (xs[0] >= qlb)
         gqp[0] += net.upper_solve(np.ones(N), gx0)
     p_is_scalar = np.ndim(r.p) == 0
-    return dict(n=gn, q_spatial=gq, p_spatial=(gp.sum() if p_is_scalar else gp), qprime=gqp, lam0=lam)
+    return dict(n=gn, q_spatial=gq, p_spatial=(gp.sum() if p_is_scalar else gp), qprime=gqp, lam0=lam, q0=g0)
 
 
 def param_grads_from_unit(gn, gq, gp, u_n, u_q, u_p, ranges, log_space=("p_spatial",)):

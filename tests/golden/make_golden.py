@@ -21,6 +21,10 @@ Fixtures:
                     12 gauge subsets (nested gauges, a headwater gauge, a gauge missing from the store)
   deep.npz      F10 the reference on C5's 281k-reach, 2215-deep basin over 24 h: unit-parameter
                     gradients and the outlet series (fp32 gradient accuracy along deep chains)
+  state.npz     F11 state gradients (route_timestep is differentiable w.r.t. q_prime_clamp and
+                    _discharge_t, mmc.py:487-559; the hot start w.r.t. q'[0], mmc.py:25-66): dL/dstreamflow
+                    of a hot-started forward, dL/dstreamflow + dL/dQ0 of a gauge-mode carried batch (one
+                    gauge's carried sum below q_lb), and a 3-step route_timestep chain
   daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
                     downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
                     warmup 3, and torch autograd's d loss / d runoff
@@ -374,10 +378,87 @@ def make_deep():
                         ref_outlet=res["runoff"][c.n - 1], **{f"ref_{k}": v for k, v in res.items() if k.startswith("grad_")})
 
 
+def make_state():
+    """F11: gradients w.r.t. the lateral inflow and the carried discharge state from the reference's
+    autograd (the fused kernel's state-gradient adjoint must reproduce them)."""
+    _, mmc = load_reference()
+    net = synthetic.random_binary_tree(90, seed=21)
+    T = 24
+    attrs = synthetic.reach_attributes(net.n, 21)
+    u = synthetic.unit_parameters(net.n, 21)
+    rng = np.random.default_rng(2100)
+    out = dict(n=np.int64(net.n), rows=net.rows, cols=net.cols, length=attrs.length, slope=attrs.slope, x=attrs.x,
+               **{f"u_{k}": v for k, v in u.items()})
+
+    def run(qprime, W, outflow_idx=None, q0=None):
+        dc = routing_dc(net.n, net.rows, net.cols, attrs, outflow_idx)
+        mc = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+        q0t = None
+        if q0 is not None:
+            q0t = torch.from_numpy(q0).clone().requires_grad_(True)
+            mc._discharge_t = q0t
+        sp_params = {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in u.items()}
+        qp = torch.from_numpy(qprime).clone().requires_grad_(True)
+        mc.setup_inputs(dc, qp, sp_params, carry_state=q0 is not None)
+        o = mc.forward()
+        (o * torch.from_numpy(W)).sum().backward()
+        r = dict(runoff=o.detach().numpy(), grad_qprime=qp.grad.numpy().copy(),
+                 **{f"grad_{k}": v.grad.numpy().copy() for k, v in sp_params.items()})
+        if q0t is not None:
+            r["grad_q0"] = q0t.grad.numpy().copy()
+        return r
+
+    # (a) hot-started forward (per-reach outputs); a few q' below the clamp
+    qa = synthetic.lateral_inflow(net.n, T, 21)
+    qa[3, :7] = 2e-5
+    hw = np.setdiff1d(np.arange(net.n), net.rows)[:3]
+    qa[0, hw] = 1e-6  # headwaters whose hot start falls below q_lb (the clamp's backward masks them)
+    Wa = rng.uniform(0, 1, (net.n, T)).astype(np.float32)
+    ra = run(qa, Wa)
+    out.update(qprime_a=qa, W_a=Wa, **{f"ref_a_{k}": v for k, v in ra.items()})
+    # (b) gauge mode with a carried state: gauge 2 is one reach whose carried Q0 is below q_lb
+    outflow = [np.array([-1]), np.array([10, 20, 31]), np.array([44]), np.array([5, 59, 60])]
+    qb = synthetic.lateral_inflow(net.n, T, 22)
+    q0 = rng.uniform(0.5, 5.0, net.n).astype(np.float32)
+    q0[44] = 3e-5
+    q0[20] = 5e-5
+    Wb = rng.uniform(0, 1, (len(outflow), T)).astype(np.float32)
+    rb = run(qb, Wb, outflow, q0)
+    flat = np.concatenate(outflow)
+    offs = np.cumsum([0] + [len(o) for o in outflow])
+    out.update(qprime_b=qb, W_b=Wb, q0_b=q0, outflow_flat=flat, outflow_offsets=offs,
+               **{f"ref_b_{k}": v for k, v in rb.items()})
+    # (c) three chained route_timestep calls (the BMI update, bmi.py -> mmc.route_timestep)
+    dc = routing_dc(net.n, net.rows, net.cols, attrs)
+    mc = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+    sp_params = {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in u.items()}
+    qc = synthetic.lateral_inflow(net.n, 3, 23)
+    mc.setup_inputs(dc, torch.from_numpy(qc), sp_params)
+    q0c = rng.uniform(0.5, 5.0, net.n).astype(np.float32)
+    s0 = torch.from_numpy(q0c).clone().requires_grad_(True)
+    mc._discharge_t = s0
+    mapper, _, _ = mc.create_pattern_mapper()
+    Wc = rng.uniform(0, 1, (3, net.n)).astype(np.float32)
+    qcl = [torch.from_numpy(np.maximum(qc[k], np.float32(1e-4))).clone().requires_grad_(True) for k in range(3)]
+    loss = 0.0
+    states = []
+    for k in range(3):
+        q1 = mc.route_timestep(q_prime_clamp=qcl[k], mapper=mapper)
+        mc._discharge_t = q1
+        states.append(q1.detach().numpy().copy())
+        loss = loss + (q1 * torch.from_numpy(Wc[k])).sum()
+    loss.backward()
+    out.update(qprime_c=qc, q0_c=q0c, W_c=Wc, ref_c_states=np.stack(states), ref_c_grad_q0=s0.grad.numpy().copy(),
+               ref_c_grad_qclamp=np.stack([q.grad.numpy().copy() for q in qcl]),
+               **{f"ref_c_grad_{k}": v.grad.numpy().copy() for k, v in sp_params.items()})
+    np.savez_compressed(HERE / "state.npz", **out)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
-            {"geostats": make_geostats, "daily": make_daily, "collate": make_collate, "deep": make_deep}[name]()
+            {"geostats": make_geostats, "daily": make_daily, "collate": make_collate, "deep": make_deep,
+             "state": make_state}[name]()
         return
     torch.manual_seed(0)
     utils, mmc = load_reference()
@@ -429,6 +510,7 @@ def main():
                         c1_mapidx=c5[4])
     make_geostats()
     make_daily()
+    make_state()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

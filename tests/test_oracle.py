@@ -133,3 +133,78 @@ def test_daily_objective_oracle_matches_reference_golden():
     assert maxrel(daily, d["ref_daily"]) <= 1e-6
     assert abs(loss - float(d["ref_loss"])) <= 1e-6 * abs(float(d["ref_loss"]))
     assert maxrel(grad, d["ref_grad"], floor=1e-12) <= 1e-6
+
+
+def _state_case():
+    from conftest import Case
+
+    d = load_golden("state")
+    u = {k: d[f"u_{k}"] for k in ("n", "q_spatial", "p_spatial")}
+    case = Case(int(d["n"]), d["rows"], d["cols"], d["length"], d["slope"], d["x"], d["qprime_a"], d["W_a"], u,
+                PARAMS_DEFAULT)
+    return case, d
+
+
+def route_timestep_chain(net, r, bd, q0, qclamp, W):
+    """The reference's BMI update (mmc.py:487-559) chained K times: loss = sum_k W_k . Q_{k+1}; returns
+    (states, dL/dQ0, dL/dq_prime_clamp (K, N), physical parameter gradients summed over the steps)."""
+    K = qclamp.shape[0]
+    states, xs = [], []
+    s = np.asarray(q0, np.float64)
+    for k in range(K):
+        qp = np.stack([qclamp[k], qclamp[k]]).astype(np.float64)
+        res = O.route(net, r, qp, bd, q0=s, dtype=np.float64)
+        xs.append(res["x"])
+        s = res["q_last"]
+        states.append(s)
+    g_state = np.zeros(net.n)
+    gq = np.zeros((K, net.n))
+    gpar = {"n": 0.0, "q_spatial": 0.0, "p_spatial": 0.0}
+    for k in range(K - 1, -1, -1):
+        G = np.zeros((net.n, 2))
+        G[:, 1] = W[k] + g_state
+        qp = np.stack([qclamp[k], qclamp[k]]).astype(np.float64)
+        bw = O.route_backward(net, r, qp, xs[k], G, bd, want_qprime=True, carry=True)
+        g_state = bw["q0"]
+        gq[k] = bw["qprime"][0] + bw["qprime"][1]
+        for key in gpar:
+            gpar[key] = gpar[key] + bw[key]
+    return np.stack(states), g_state, gq, gpar
+
+
+def test_oracle_state_gradients_match_reference():
+    """dL/dq' (incl. the hot start's) and dL/dQ0 (carried state, gauge mode with a gauge sum below
+    q_lb), and a route_timestep chain, against the reference's autograd (F11)."""
+    case, d = _state_case()
+    net, r, bd = case.network(), case.reaches(), case.bounds
+    # (a) hot-started forward: dL/dstreamflow
+    res = O.route(net, r, d["qprime_a"], bd, dtype=np.float64)
+    assert maxrel(res["runoff"], d["ref_a_runoff"]) < FWD_TOL
+    bw = O.route_backward(net, r, d["qprime_a"], res["x"], d["W_a"], bd, want_qprime=True)
+    assert normrel(bw["qprime"], d["ref_a_grad_qprime"]) < GRAD_TOL
+    assert maxrel(bw["qprime"][0], d["ref_a_grad_qprime"][0], 1e-3) < 1e-4   # the hot start row
+    assert np.all(bw["qprime"][-1] == 0) and np.all(d["ref_a_grad_qprime"][-1] == 0)
+    # (b) gauge mode, carried state
+    offs = d["outflow_offsets"]
+    outflow = [d["outflow_flat"][offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    res = O.route(net, r, d["qprime_b"], bd, q0=d["q0_b"], dtype=np.float64, outflow_idx=outflow)
+    assert maxrel(res["runoff"], d["ref_b_runoff"]) < FWD_TOL
+    bw = O.route_backward(net, r, d["qprime_b"], res["x"], d["W_b"], bd, outflow_idx=outflow, want_qprime=True,
+                          carry=True)
+    assert normrel(bw["qprime"], d["ref_b_grad_qprime"]) < GRAD_TOL
+    assert normrel(bw["q0"], d["ref_b_grad_q0"]) < GRAD_TOL
+    assert d["ref_b_grad_q0"][44] != 0.0  # Q0 below q_lb still feeds step 1 unclamped
+    g = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], case.u["n"], case.u["q_spatial"],
+                                case.u["p_spatial"], case.params["parameter_ranges"])
+    for k, v in g.items():
+        assert normrel(v, d[f"ref_b_grad_{k}"]) < GRAD_TOL, k
+    # (c) route_timestep chain
+    qcl = np.maximum(d["qprime_c"], np.float32(1e-4))
+    states, g0, gq, gpar = route_timestep_chain(net, r, bd, d["q0_c"], qcl, d["W_c"])
+    assert maxrel(states, d["ref_c_states"]) < FWD_TOL
+    assert normrel(g0, d["ref_c_grad_q0"]) < GRAD_TOL
+    assert normrel(gq, d["ref_c_grad_qclamp"]) < GRAD_TOL
+    g = O.param_grads_from_unit(gpar["n"], gpar["q_spatial"], gpar["p_spatial"], case.u["n"], case.u["q_spatial"],
+                                case.u["p_spatial"], case.params["parameter_ranges"])
+    for k, v in g.items():
+        assert normrel(v, d[f"ref_c_grad_{k}"]) < GRAD_TOL, k
