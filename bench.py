@@ -560,6 +560,20 @@ def block_profile(path, g, step, lib):
         log(f"[profile] {key}: end min/median/max {e.min():.0f}/{np.median(e):.0f}/{e.max():.0f} us, "
             f"wait max {p[:, 2].max() / 100:.0f} us")
     out["nloc"] = sizes.tolist()
+    # per-block structure: cut edges in / out, basins, whether a basin spans blocks, depth span
+    blk, down, basin, dist = s["block"], s["down"], s["basin"], s["dist"]
+    has = down >= 0
+    src, dst = np.flatnonzero(has), down[has]
+    cut = blk[src] != blk[dst]
+    out["cut_in"] = np.bincount(blk[dst[cut]], minlength=nb).tolist()
+    out["cut_out"] = np.bincount(blk[src[cut]], minlength=nb).tolist()
+    nblk_of_basin = np.bincount(np.unique(np.stack([basin, blk]), axis=1)[0])
+    out["split"] = np.bincount(blk, weights=(nblk_of_basin[basin] > 1), minlength=nb).tolist()
+    dmin = np.full(nb, np.iinfo(np.int64).max)
+    np.minimum.at(dmin, blk, dist)
+    dmx = np.zeros(nb, np.int64)
+    np.maximum.at(dmx, blk, dist)
+    out["dist_span"] = (dmx - dmin).tolist()
     Path(path).parent.mkdir(parents=True, exist_ok=True)
     Path(path).write_text(json.dumps(out))
 

@@ -37,6 +37,12 @@ namespace ddr {
 #ifndef DDR_BWD_EXACT
 #define DDR_BWD_EXACT 0
 #endif
+#ifndef DDR_BWD_EARLY_LOADS
+#define DDR_BWD_EARLY_LOADS 1
+#endif
+#ifndef DDR_BWD_EARLY_MAX_KR
+#define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
+#endif
 
 namespace {
 
@@ -678,6 +684,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
   // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
   R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  // early loads (DDR_BWD_EARLY_LOADS): the next tick's x(t - 3) and virtual x are requested at the top
+  // of the tick into a second register set (roles swap every tick: the loop is unrolled by two), so
+  // they have the whole tick to land instead of the part after the first barrier
+  R xb2[KR];
+  constexpr bool kEarly = DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR;
   R qsv[GS ? KR : 1];  // state gradients: q' * flow_scale of this tick's step (prefetched a tick ahead)
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
@@ -793,9 +804,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   // virtual inflow's x(t_v - 2), prefetched one tick ahead (kept as loaded: converting it would
   // wait for the load in the tick that issues it)
-  double vx = 0.0;
+  double vx = 0.0, vx2 = 0.0;
 
-  auto tick = [&](int tb) {
+  // xbc / vxc: loaded last tick, published now; xbn / vxn: loaded now for the next tick (the same
+  // registers without early loads)
+  auto tick = [&](int tb, R(&xbc)[KR], R(&xbn)[KR], double& vxc, double& vxn) {
     const int tau = TT - 1 - tb;  // forward tick
     // Every global load of the previous tick (states, virtual inflows, gradient groups) lands
     // here, a whole tick after its issue.  An explicit wait the compiler can see: without it, its
@@ -809,6 +822,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       ref[k] = opq(ref[k]);
       od[k] = opq(od[k]);
       up[k] = opq(up[k]);
+    }
+    if constexpr (kEarly) {
+      load_own(tau - 3, xbn, tq);                                  // x(t - 3), published next tick
+      if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);      // the virtual's value for the next tick
     }
     if (B.ncout > 0 && (tb % kChunk) == 0) {
       // one (cut-out, step) per thread and iteration, its (A, B) granule pair requested together; the
@@ -843,7 +860,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
         store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
       }
-      sx[B.nloc + tid] = R(vx);
+      sx[B.nloc + tid] = R(vxc);
     }
     R A[KR], Bd[KR];
 #pragma unroll
@@ -852,7 +869,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       Bd[k] = R(0);
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
-      if (r < B.nloc) sx[r] = xb[k];  // x(t - 2): the upstream value of the downstream reach's step t - 1
+      if (r < B.nloc) sx[r] = xbc[k];  // x(t - 2): the upstream value of the downstream reach's step t - 1
       const int dl = dl_of(k);
       if (dl >= 0) {
         A[k] = sa[dl];
@@ -866,8 +883,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     phz.mark(2);  // read / publish
     lds_barrier();
     phz.mark(3);  // barrier 1
-    load_own(tau - 3, xb, tq);                    // x(t - 3), published next tick
-    if (vown) vx = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
+    if constexpr (!kEarly) {
+      load_own(tau - 3, xbn, tq);                    // x(t - 3), published next tick
+      if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
+    }
     // ---- compute ------------------------------------------------------------------------------
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -1019,10 +1038,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
   phz.start();
+  if constexpr (kEarly) {
 #pragma unroll 1
-  for (int tb = 0; tb < TT; ++tb) {
-    if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
-    tick(tb);
+    for (int tb = 0; tb < TT; tb += 2) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb2, vx, vx2);
+      if (tb + 1 < TT) tick(tb + 1, xb2, xb, vx2, vx);
+    }
+  } else {
+#pragma unroll 1
+    for (int tb = 0; tb < TT; ++tb) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb, vx, vx);
+    }
   }
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
   phz.flush(a.prof, a.nblocks, bid);

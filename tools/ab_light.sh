@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of library variants at a light load (100k reaches) and on C5: VARIANT names (base = libddr_mc.so).
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-abl}
+mkdir -p $OUT
+for size in light c5; do
+  for v in "$@"; do
+    lib=$R/ddr_amd/lib/libddr_mc_$v.so; [ "$v" = base ] && lib=$R/ddr_amd/lib/libddr_mc.so
+    fl=""; [ $size = light ] && fl="--reaches 100000 --basins 400"
+    DDR_MC_LIB=$lib timeout -k 10 200 python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps 0 $fl > $OUT/${v}_$size.log 2>&1 || { echo "$v $size failed"; tail -3 $OUT/${v}_$size.log; exit 1; }
+    echo "$v $size" $(grep '^{' $OUT/${v}_$size.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['ms_per_step'],1), {k: round(v['kernel_ms'],2) for k, v in d['kernels'].items()})")
+  done
+done
