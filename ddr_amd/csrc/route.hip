@@ -40,6 +40,15 @@ namespace ddr {
 #ifndef DDR_BWD_EARLY_LOADS
 #define DDR_BWD_EARLY_LOADS 1
 #endif
+// Skip the physics of a wave-slice none of whose lanes runs a step in this tick.  Forward: C3 -7 %,
+// C5 -2 %, route_timestep 9.2 -> 3.5 ms at 800k; backward: no gain measured (+0.8 % C5), off
+// (profiles/r02/ab_defer_early.txt)
+#ifndef DDR_SKIP_IDLE
+#define DDR_SKIP_IDLE 1
+#endif
+#ifndef DDR_SKIP_IDLE_BWD
+#define DDR_SKIP_IDLE_BWD 0
+#endif
 #ifndef DDR_BWD_EARLY_MAX_KR
 #define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
 #endif
@@ -477,6 +486,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k0 = 0; k0 < KR; k0 += NP) {
       if (wbase + k0 * BS >= B.nloc) continue;
+      if (DDR_SKIP_IDLE) {
+        // no lane of the wave runs a step this tick (before its first / after its last step: the
+        // first and last dmax ticks of a block, most ticks of a short window): skip the slice
+        bool act = false;
+#pragma unroll
+        for (int h = 0; h < NP; ++h) {
+          const int t = tau - off_of(k0 + h);
+          act = act || (tq + (k0 + h) * BS < B.nloc && t >= 0 && t < T);
+        }
+        if (__builtin_amdgcn_ballot_w64(act) == 0) continue;
+      }
       ReachStatic<R> st[NP];
       R Qv[NP];
       PhysOut<R> ph[NP];
@@ -927,6 +947,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
       const R gb = R(gb64);
       const R Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);     // Q_{t-1}
+      // the step's adjoint only where some lane of the wave runs a step this tick (DDR_SKIP_IDLE_BWD)
+      const bool wave_act = !DDR_SKIP_IDLE_BWD || __builtin_amdgcn_ballot_w64(active || (GS && hk && t == 0)) != 0;
+      if (wave_act) {
       R c1, c2, c3, c4, gQ, gn, gq, gp;
       if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
         const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
@@ -974,6 +997,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           sb[r] = R(0);
         }
       }
+      }  // wave_act
       if constexpr (GS) {
         const int tn = tau > 0 ? tau - 1 : 0;  // the next backward tick's row
         qsv[k] = qsp[xs_base + (int64_t)tn * B.nloc + rs];
