@@ -35,10 +35,19 @@ constexpr int kMinBlockCap = DDR_MIN_BLOCK_CAP;
 constexpr size_t kLdsBudget = 160 * 1024 / kBlocksPerCU - 512;
 // Chunk of ticks between two inter-workgroup imports (SURVEY §7 "time-pipelined").  Every
 // block-DAG hop adds about one chunk of lag, so the chunk is short.
-#ifndef DDR_CHUNK
-#define DDR_CHUNK 8
+// Forward and backward chunks differ (A/B, profiles/r02/ab_defer_early.txt: forward 4 beats 8 and 16;
+// the backward's import is a workgroup-wide step, 8 kept).  The forward's must be a multiple of the
+// import batch (4).
+#ifndef DDR_CHUNK_FWD
+#define DDR_CHUNK_FWD 4
 #endif
-constexpr int kChunk = DDR_CHUNK;
+#ifndef DDR_CHUNK_BWD
+#define DDR_CHUNK_BWD 8
+#endif
+constexpr int kChunkFwd = DDR_CHUNK_FWD;
+constexpr int kChunkBwd = DDR_CHUNK_BWD;
+// the packer's lag estimate per block-DAG hop (graph.cpp)
+constexpr int kChunk = 8;
 // Parameter-gradient partial sums are flushed to the fp64 accumulators every kGradFlush steps
 // (aligned to the step index, so the summation grouping does not depend on the partition).
 constexpr int kGradFlush = 128;
@@ -48,8 +57,8 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16;
 __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_slots + 2) & ~1; }
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
-//   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunk] f64
-//   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunk][2] (R)
+//   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunkFwd] f64
+//   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunkBwd][2] (R)
 //             | owner words
 // and then the block's confluence lists (after the math tables of fastmath.h, which occupy the first
 // kMathTabBytes)
@@ -60,7 +69,7 @@ constexpr int kMaxConfluenceList = 8191;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nvirt, size_t ncout, size_t nxl, bool backward,
                                                   size_t rsize) {
   const size_t base = backward ? slots * 9 * rsize : slots * (8 + 6 * rsize);
-  const size_t ring = backward ? ncout * kChunk * 2 * rsize : nvirt * kChunk * 8;
+  const size_t ring = backward ? ncout * kChunkBwd * 2 * rsize : nvirt * kChunkFwd * 8;
   // backward: per hand-off owner thread (tid < max(nvirt, ncout)) its virtual's downstream slot and
   // its cut-out's tick offset
   const size_t own = backward ? align16(4 * (nvirt > ncout ? nvirt : ncout)) : 0;

@@ -8,7 +8,7 @@
 // ("as late as possible" wavefront; T + dmax ticks instead of T x depth level syncs).
 // Edges between blocks (cut edges) are exchanged through global memory as 8-byte granules that
 // are their own ready flag (sentinel = all ones, re-initialised before every launch), imported in
-// chunks of kChunk ticks so the hand-off latency is paid once per chunk.
+// chunks of kChunkFwd / kChunkBwd ticks so the hand-off latency is paid once per chunk.
 //
 // Workgroups take their logical block from a ticket counter (take_ticket): blocks are numbered in
 // piece-height order, so the producers of a running workgroup were taken by workgroups that are
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int S = a.slot_stride;
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
   const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
-  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunk]
+  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunkFwd]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
   const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith);
   const int64_t T = a.T;
@@ -456,18 +456,18 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       ex[k] = opq(ex[k]);
       inv[k] = opq(inv[k]);
     }
-    if (B.nvirt > 0 && (tau % kChunk) == 0) {
+    if (B.nvirt > 0 && (tau % kChunkFwd) == 0) {
       // import the next chunk of every virtual inflow (x of the upstream block's reach): its owner
-      // thread requests the kChunk granules at once
+      // thread requests the kChunkFwd granules at once
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
       if (vown) {
 #pragma unroll
-        for (int h = 0; h < kChunk; h += kImportBatch) {
+        for (int h = 0; h < kChunkFwd; h += kImportBatch) {
           double g[kImportBatch];
           wait_granules<kImportBatch>(a.bnd + (int64_t)v_edge * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status, bid,
                                       force_to);
 #pragma unroll
-          for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunk + h + i] = g[i];
+          for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunkFwd + h + i] = g[i];
         }
       }
 #ifndef DDR_FWD_IMPORT_BARRIER
@@ -602,7 +602,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     }
     if (vown) {
       const int t = tau - v_off;
-      if (t >= 0 && t < T) sx[B.nloc + vi] = ring[vi * kChunk + (tau % kChunk)];
+      if (t >= 0 && t < T) sx[B.nloc + vi] = ring[vi * kChunkFwd + (tau % kChunkFwd)];
     }
     phz.mark(4);  // publish
     lds_barrier();
@@ -676,7 +676,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   R* sb = sa + S;                                       // [S] c2_i gb_i (adjoint of the inflow)
   R* sx = sb + S;                                       // [S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
   const StatTab<R> tab{sx + S};                         // [S][6]
-  R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * 9 * sizeof(R)));  // [ncout][kChunk][2]
+  R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * 9 * sizeof(R)));  // [ncout][kChunkBwd][2]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                                            // confluence lists
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
@@ -847,13 +847,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       load_own(tau - 3, xbn, tq);                                  // x(t - 3), published next tick
       if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);      // the virtual's value for the next tick
     }
-    if (B.ncout > 0 && (tb % kChunk) == 0) {
+    if (B.ncout > 0 && (tb % kChunkBwd) == 0) {
       // one (cut-out, step) per thread and iteration, its (A, B) granule pair requested together; the
       // cut edge of cut-out c is B.cout0 + c (graph.cpp numbers cut edges in block order), its tick
       // offset is in the owner words
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-      for (int w = tid; w < B.ncout * kChunk; w += BS) {
-        const int c = w / kChunk, sidx = w % kChunk;
+      for (int w = tid; w < B.ncout * kChunkBwd; w += BS) {
+        const int c = w / kChunkBwd, sidx = w % kChunkBwd;
         const int t = (tau - sidx) - (int)(own[c] >> 16);
         R A = R(0), Bv = R(0);
         if (t >= tmin && t < T) {
@@ -862,8 +862,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           A = R(g[0]);
           Bv = R(g[1]);
         }
-        ring[(c * kChunk + sidx) * 2] = A;
-        ring[(c * kChunk + sidx) * 2 + 1] = Bv;
+        ring[(c * kChunkBwd + sidx) * 2] = A;
+        ring[(c * kChunkBwd + sidx) * 2 + 1] = Bv;
       }
       lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
@@ -895,9 +895,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         A[k] = sa[dl];
         Bd[k] = sb[dl];
       } else if (dl <= -2) {
-        const int sidx = tb % kChunk;
-        A[k] = ring[((-dl - 2) * kChunk + sidx) * 2];
-        Bd[k] = ring[((-dl - 2) * kChunk + sidx) * 2 + 1];
+        const int sidx = tb % kChunkBwd;
+        A[k] = ring[((-dl - 2) * kChunkBwd + sidx) * 2];
+        Bd[k] = ring[((-dl - 2) * kChunkBwd + sidx) * 2 + 1];
       }
     }
     phz.mark(2);  // read / publish
