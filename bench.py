@@ -206,7 +206,11 @@ def main():
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
     dist = None
-    if world > 1:
+    # DDR_BENCH_ALONE=1 (strong-scaling prediction on one GPU, tools/scale_alone.sh): run rank RANK's
+    # shard of WORLD_SIZE alone, without a process group -- the shards share nothing on the data path,
+    # so a rank's step time is its shard's time (plus the latency-bound gradient all-reduce)
+    alone = os.environ.get("DDR_BENCH_ALONE") == "1"
+    if world > 1 and not alone:
         import torch.distributed as dist
 
         backend = os.environ.get("DDR_DIST_BACKEND", "nccl")
@@ -345,7 +349,7 @@ def main():
     total_reaches = int(sizes.sum())
     value = total_reaches * (T - 1) * args.steps / elapsed
 
-    if rank == 0:
+    if rank == 0 or alone:
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         reach_steps = n_loc * (T - 1)
         kern = {}

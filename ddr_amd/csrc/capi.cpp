@@ -148,6 +148,7 @@ void fill_common(RouteArgs& a, const Graph* g, const ddr_mc_consts* c, const ddr
   a.qp_hours = r->qprime_hours > 1 ? (int32_t)r->qprime_hours : 1;
   a.qp_shift = (flags & DDR_FWD_ACCUMULATE) ? 0 : 1;
   a.qp_valid = r->qprime_valid;
+  choose_qs_layout(a);  // needs T, qp_hours, qp_shift
   a.qprime = qprime;
   a.c[0] = c->dt;
   a.c[1] = c->discharge_lb;

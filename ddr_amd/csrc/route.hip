@@ -313,6 +313,22 @@ struct StatTab {
   }
 };
 
+// The gathered q' * flow_scale of local position r running step t = tau - off at forward tick tau:
+// the tick-major schedule layout (row tau), or the row layout of a multi-hour store (choose_qs_layout).
+template <typename R>
+__device__ __forceinline__ const R* qs_at(const RouteArgs& a, const BlockDesc& B, int64_t xs_base, int tau, int off,
+                                          int r) {
+  const R* qs = static_cast<const R*>(a.qs);
+  if (a.qs_rows > 0) {
+    int t = tau - off;
+    t = t < 0 ? 0 : (t >= (int)a.T ? (int)a.T - 1 : t);
+    t = t > a.qp_shift ? t - a.qp_shift : 0;
+    const unsigned row = __umulhi((unsigned)t, a.qp_magic);  // t / qp_hours
+    return qs + (int64_t)a.qs_rows * B.pos0 + (int64_t)row * B.nloc + r;
+  }
+  return qs + xs_base + (int64_t)tau * B.nloc + r;
+}
+
 // ============================================================================================
 // Forward
 // ============================================================================================
@@ -429,13 +445,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // q'[max(t-1,0)] * flow_scale (gathered into the schedule layout: one row per tick), or the
   // carried Q0 at t = 0, for the step each reach runs at tick `tau`
   const R* qsb = static_cast<const R*>(a.qs) + xs_base;
+  const bool qs_rows = a.qs_rows > 0;
   auto prefetch = [&](int tau, R(&dst)[KR], int tq0) {
     const R* row = qsb + (int64_t)(tau < TTf ? tau : TTf - 1) * B.nloc;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq0 + k * BS;
-      dst[k] = (carry && tau == off_of(k)) ? q0p[ref[k]] : row[r < B.nloc ? r : 0];
+      const int rs = r < B.nloc ? r : 0;
+      const R v = qs_rows ? *qs_at<R>(a, B, xs_base, tau, off_of(k), rs) : row[rs];
+      dst[k] = (carry && tau == off_of(k)) ? q0p[ref[k]] : v;
     }
   };
 
@@ -689,7 +708,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
   const int tmin = GS ? 0 : 1;                  // first step of the sweep (step 0: the hot start / Q0)
   R* gqs = static_cast<R*>(a.gqs);
-  const R* qsp = static_cast<const R*>(a.qs);
 
   // od packs the tick offset (bits 16-30), dl (low 16, signed): local downstream (>= 0),
   // -(import slot + 2), or -1, and bit 31: the reach has no dL/drunoff row (gauge mode, ungauged
@@ -955,7 +973,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
         c1 = o.c1; c2 = o.c2; c3 = o.c3; c4 = o.c4; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
       } else {
-        const R qvk = static_cast<const R*>(a.qs)[xs_base + (int64_t)tau * B.nloc + rs];  // q'[t-1] * flow_scale
+        const R qvk = *qs_at<R>(a, B, xs_base, tau, off_of(k), rs);  // q'[t-1] * flow_scale
         R tw, ss;
         Geom<R> geo;
         coefficients<R, !DDR_BWD_EXACT>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
@@ -1000,7 +1018,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }  // wave_act
       if constexpr (GS) {
         const int tn = tau > 0 ? tau - 1 : 0;  // the next backward tick's row
-        qsv[k] = qsp[xs_base + (int64_t)tn * B.nloc + rs];
+        qsv[k] = *qs_at<R>(a, B, xs_base, tn, off_of(k), rs);
       }
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
@@ -1028,7 +1046,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int r = tid + k * BS;
-      qsv[k] = qsp[xs_base + (int64_t)(TT - 1) * B.nloc + (r < B.nloc ? r : 0)];
+      qsv[k] = *qs_at<R>(a, B, xs_base, TT - 1, off_of(k), r < B.nloc ? r : 0);
     }
   }
   load_own(TT - 1, xc, tid);
@@ -1181,6 +1199,47 @@ __global__ void scatter_qprime_grad_kernel(RouteArgs a, int64_t rows, R* out) {
   if (a.qp_valid && !a.qp_valid[ref]) acc = R(0);
   if (a.fs) acc = acc * static_cast<const R*>(a.fs)[ref];
   out[w] = acc;
+}
+
+// Row layout (a store of qp_hours > 1 steps per row): per block [qs_rows][nloc], row d holds q' row d
+// of the store for every local position -- qp_hours times fewer bytes than the tick-major layout.
+template <typename R, int G>
+__global__ void __launch_bounds__(1024) gather_qprime_rows_kernel(RouteArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
+  R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
+  const BlockDesc B = a.s.blocks[blockIdx.x];
+  const int64_t N = a.N, d0 = (int64_t)blockIdx.y * G;
+  const int nl = B.nloc;
+  const R* qp = static_cast<const R*>(a.qprime);
+  const R* fs = static_cast<const R*>(a.fs);
+  const int* rs_loc = a.s.rs_loc + B.pos0;
+  const int* rs_ref = a.s.rs_ref + B.pos0;
+  const int jn = (int)(a.qs_rows - d0 < G ? a.qs_rows - d0 : G);
+  const unsigned char* valid = a.qp_valid;
+  for (int i = threadIdx.x; i < nl; i += 1024) {
+    const int ref = rs_ref[i], loc = rs_loc[i];
+    R v[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) v[j] = j < jn ? qp[(d0 + j) * N + ref] : R(0);
+    if (valid && !valid[ref]) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) v[j] = R(0.001f);  // readers.py:523-530
+    }
+    if (fs) {
+      const R f = fs[ref];
+#pragma unroll
+      for (int j = 0; j < G; ++j) v[j] = v[j] * f;
+    }
+#pragma unroll
+    for (int j = 0; j < G; ++j) tile[j * nl + loc] = v[j];
+  }
+  __syncthreads();
+  R* qs = static_cast<R*>(a.qs) + (int64_t)a.qs_rows * B.pos0;
+  for (int r = threadIdx.x; r < nl; r += 1024) {
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (j < jn) qs[(d0 + j) * nl + r] = tile[j * nl + r];
+  }
 }
 
 // ============================================================================================
@@ -1348,6 +1407,14 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
 #endif
   constexpr int G = sizeof(R) == 4 ? DDR_GATHER_G : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
   const size_t smem = (size_t)G * g->max_nloc * sizeof(R);
+  if (a.qs_rows > 0) {
+    auto rk = gather_qprime_rows_kernel<R, G>;
+    hipError_t e = hipFuncSetAttribute((const void*)rk, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rk, dim3((unsigned)g->blocks.size(), (unsigned)((a.qs_rows + G - 1) / G)), dim3(1024), smem,
+                       stream, a);
+    return hipGetLastError();
+  }
   auto kern = gather_qprime_kernel<R, G>;
   hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;

@@ -17,6 +17,11 @@ struct RouteArgs {
   int32_t p_stride;
   int32_t qp_hours;               // hourly steps per stored q' row (1, or 24 for a daily store)
   int32_t qp_shift;               // step t reads q' row max(t - qp_shift, 0): 1 routing, 0 accumulation
+  // row layout of the gathered q' (a store of qp_hours > 1 steps per row, e.g. daily): per block
+  // [qp_rows][nloc] instead of the tick-major [T + dmax][nloc]; row = max(t - shift, 0) / qp_hours,
+  // the division as a multiply-high by qp_magic (exact for the window, checked on the host)
+  int32_t qs_rows;                // 0: tick-major layout; else rows per block of the row layout
+  uint32_t qp_magic;
   const unsigned char* qp_valid;  // optional per-reach mask: 0 -> q' = 0.001 (missing divide)
   const void* n;
   const void* q;
@@ -79,6 +84,24 @@ template <typename R>
 int max_resident_blocks(const Graph* g, bool backward);
 template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream);
+// Sets a.qs_rows / a.qp_magic when the window's q' store has several steps per row and the
+// row layout's magic division is exact over the window (otherwise the tick-major layout).
+inline void choose_qs_layout(RouteArgs& a) {
+  a.qs_rows = 0;
+  a.qp_magic = 0;
+  const int64_t H = a.qp_hours;
+#ifndef DDR_QS_ROWS
+#define DDR_QS_ROWS 1
+#endif
+  if (!DDR_QS_ROWS || H <= 1 || a.T < 1) return;
+  const uint64_t m = ((uint64_t(1) << 32) + (uint64_t)H - 1) / (uint64_t)H;  // ceil(2^32 / H)
+  const uint64_t err = m * (uint64_t)H - (uint64_t(1) << 32);
+  // floor(t m / 2^32) == floor(t / H) for t * err < 2^32 / H
+  if (err > 0 && (uint64_t)a.T * err >= ((uint64_t(1) << 32) / (uint64_t)H)) return;
+  const int64_t last = a.T - 1 > a.qp_shift ? a.T - 1 - a.qp_shift : 0;
+  a.qs_rows = (int32_t)(last / H + 1);
+  a.qp_magic = (uint32_t)m;
+}
 template <typename R>
 hipError_t launch_gauge(const GaugeArgs& a, const R* xsave, R* out, hipStream_t stream);
 template <typename R>
