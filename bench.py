@@ -358,7 +358,7 @@ def main():
     elapsed = time.perf_counter() - t0
     _lib.check(lib.ddr_set_kernel_timing(0))
     _lib.check(lib.ddr_status_check(1))  # any timed-out hand-off fails the run
-    if args.block_profile and rank == 0:
+    if args.block_profile and (rank == 0 or alone):
         block_profile(args.block_profile, g, step, lib)
 
     # ---- reductions over ranks ------------------------------------------------------------------------
