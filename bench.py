@@ -286,7 +286,7 @@ def main():
 
         feats = tt(synthetic.reach_features(net.n, seed=11))
         model = ParamNet().to(dev)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)  # one launch per step, not per tensor
         # one gauge per subnetwork outlet; observations indexed by the gauge's global number
         outlets_global = np.flatnonzero(net.down < 0)
         outlets = np.flatnonzero(np.isin(ids, outlets_global))
@@ -307,7 +307,7 @@ def main():
             loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
             loss.backward()
             allreduce_gradients(list(model.parameters()))  # RCCL, one flat bucket
-            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0, foreach=True)
             opt.step()
 
     else:
@@ -464,7 +464,7 @@ def time_training_stream(args, dev):
     log(f"[stream] {M} batches resident in {time.perf_counter() - t_gen:.1f}s "
         f"({min(d['net'].n for d in data)}..{max(d['net'].n for d in data)} reaches)")
     model = ParamNet().to(dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     wd = args.warmup_days
     consts = RouteConsts()
     torch.cuda.synchronize()
@@ -489,7 +489,7 @@ def time_training_stream(args, dev):
         loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])
         loss.backward()
         allreduce_gradients(list(model.parameters()))
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0, foreach=True)
         opt.step()
         if k >= warm:
             per.append({"reaches": int(d["net"].n), "generations": g.info.generations, "blocks": g.info.n_blocks,

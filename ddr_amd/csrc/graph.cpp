@@ -156,6 +156,19 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   // cheapest spread thin over many workgroups, not packed into a few full ones.
   const int64_t min_cap = std::min<int64_t>(kMinBlockCap, bs);
   int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(min_cap, (n + target - 1) / target));
+  // ... rounded up to whole slices per SIMD (4 x 64 reaches) at light and medium loads: a tick costs
+  // per slice on the busiest SIMD, so the rounding keeps that cost and makes fewer, larger pieces --
+  // fewer cut edges and shorter block chains (routing of a C3 8-way shard 8.1 -> 7.2 ms, of C5's
+  // giant-basin shard 57.6 -> 54.3 ms); at full load (C3, C5 on one GPU) it measured slower
+  // (profiles/r02/ab_defer_early.txt)
+#ifndef DDR_CAP_QUANT
+#define DDR_CAP_QUANT 256
+#endif
+#ifndef DDR_CAP_QUANT_MAX
+#define DDR_CAP_QUANT_MAX 2048
+#endif
+  if (DDR_CAP_QUANT > 1 && cap <= DDR_CAP_QUANT_MAX)
+    cap = std::min<int64_t>(hard_cap, (cap + DDR_CAP_QUANT - 1) / DDR_CAP_QUANT * DDR_CAP_QUANT);
   const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
   // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
   const double fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
