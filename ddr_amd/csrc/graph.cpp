@@ -194,6 +194,21 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   // The packer first tries to fit one resident generation (all blocks co-resident, fully time-
   // pipelined): path-weighted packing, then unweighted; failing both it packs gen x resident
   // smaller blocks (every extra generation costs about T more ticks of the blocks it holds).
+  // Split threshold (pieces up to scap_pct % of the capacity): with a dominant basin (C4/C5: 0.35 N)
+  // its chain of pieces is the critical path, and pieces at 80 % leave the packer room to give chain
+  // blocks fewer reaches; without one (C3: 256 basins of at most 2 % of N) pieces at the full
+  // capacity mean fewer cut edges (C3 38.7 -> 36.5 ms per step; C5 at 100 %: 138 -> 149 ms;
+  // profiles/r02/ab_defer_early.txt)
+  int64_t scap_pct = 80;
+  {
+    std::vector<int32_t> bsz(n, 0);
+    int64_t bmax = 0;
+    for (int64_t i = 0; i < n; ++i) bmax = std::max<int64_t>(bmax, ++bsz[g->basin[i]]);
+    if (bmax * 10 < n) scap_pct = 100;
+#ifdef DDR_SCAP_PCT
+    scap_pct = DDR_SCAP_PCT;
+#endif
+  }
   bool weighted = true;
   int64_t gen = 1;
   const int64_t cap_start = cap;
@@ -205,7 +220,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     // least lseg reaches.  The stem child is cut only when the piece is full.
     // Pieces of split basins are kept below the block capacity: they land in blocks on long
     // chains, whose packing weight is up to ~(T + depth) / T times their size.
-    const int64_t scap = cap * 4 / 5;
+    const int64_t scap = cap * scap_pct / 100;
     const int64_t lseg = scap / 8;
     std::fill(is_root.begin(), is_root.end(), 0);
     for (int64_t i = 0; i < n; ++i) {
