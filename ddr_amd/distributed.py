@@ -24,7 +24,7 @@ def rank_world():
     return 0, 1
 
 
-def shard_network(n: int, rows: np.ndarray, cols: np.ndarray, rank: int, world: int, depth_weight: float = 0.0):
+def shard_network(n: int, rows: np.ndarray, cols: np.ndarray, rank: int, world: int):
     """This rank's sub-network: whole outlet basins, LPT-balanced by reach count.
 
     Returns (n_sub, rows_sub, cols_sub, reach_ids) with ``reach_ids`` the global reach index of each
