@@ -181,6 +181,21 @@ def test_triangular_solve_routing_matrix(cuda):
     x = triangular_sparse_solve(mapper.map(c1_), mapper.crow_indices, mapper.col_indices, b, True, False, cuda)
     ref = O.Network.from_coo(net.n, net.rows, net.cols).lower_solve(c1.cpu().numpy(), b.cpu().numpy())
     np.testing.assert_array_equal(x.cpu().numpy(), ref.astype(np.float32))
+    # the per-step API solves one pattern every step: the second call reuses the cached plan (same
+    # pattern, new values) and must give the new values' solution
+    c1b = torch.rand(net.n, device=cuda) * 0.5
+    c1b_ = c1b * -1
+    c1b_[0] = 1.0
+    x2 = triangular_sparse_solve(mapper.map(c1b_), mapper.crow_indices, mapper.col_indices, b, True, False, cuda)
+    ref2 = O.Network.from_coo(net.n, net.rows, net.cols).lower_solve(c1b.cpu().numpy(), b.cpu().numpy())
+    np.testing.assert_array_equal(x2.cpu().numpy(), ref2.astype(np.float32))
+    # other patterns in between (cache misses), then the first pattern again
+    n = 5
+    xi = triangular_sparse_solve(torch.ones(n, device=cuda), torch.arange(n + 1), torch.arange(n),
+                                 torch.arange(1.0, 6.0, device=cuda), True, False, cuda)
+    np.testing.assert_array_equal(xi.cpu().numpy(), np.arange(1.0, 6.0))
+    x3 = triangular_sparse_solve(mapper.map(c1_), mapper.crow_indices, mapper.col_indices, b, True, False, cuda)
+    np.testing.assert_array_equal(x3.cpu().numpy(), ref.astype(np.float32))
 
 
 def test_nan_streamflow_asserts_like_the_reference(cuda):
