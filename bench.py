@@ -207,6 +207,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dropin-steps", type=int, default=2, help="C5, 1 GPU: also time the drop-in dmc() path")
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
+    ap.add_argument("--grad-qprime", action="store_true",
+                    help="C5: q' requires grad, so the backward is the state-gradient adjoint (dL/dq' too)")
     ap.add_argument("--stream", type=int, default=0,
                     help="C3, 1 GPU: also time K training steps over K different batches (a new gauge-union "
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
@@ -273,9 +275,11 @@ def main():
         u_n, u_q, u_p = (tt(u[k]).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial"))
         gen = torch.Generator(device=dev).manual_seed(1234 + rank)
         W = torch.rand((n_loc, T), device=dev, dtype=torch.float32, generator=gen)  # dL/drunoff of sum(W * runoff)
+        if args.grad_qprime:
+            qprime.requires_grad_(True)
 
         def step():
-            for t_ in (u_n, u_q, u_p):
+            for t_ in (u_n, u_q, u_p, qprime):
                 t_.grad = None
             n, q, p = denorm(u_n, u_q, u_p)
             runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, math=args.math)
@@ -406,7 +410,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": spec["desc"], "reaches": total_reaches, "T": T, "qprime_store": "daily" if qp_hours == 24 else "hourly",
+            "config": {"workload": spec["desc"] + (" + dL/dq' (state-gradient adjoint)" if args.grad_qprime else ""), "reaches": total_reaches, "T": T, "qprime_store": "daily" if qp_hours == 24 else "hourly",
                        "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",
                                         "faithful": "faithful (reference op order, IEEE division, fp32 faithful-class pow)",
                                         "fast": "fast (hardware rcp/log/exp fp32)"}[args.math],
