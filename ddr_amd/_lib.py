@@ -78,7 +78,7 @@ _SIGS = {
     "ddr_graph_build": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), C.POINTER(C.c_void_p)]),
     "ddr_graph_destroy": (C.c_int, [_P]),
     "ddr_graph_upload": (C.c_int, [_P]),
-    "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "ddr_graph_get_info": (C.c_int, [_P, C.POINTER(GraphInfo)]),
     "ddr_graph_csr": (C.c_int, [_P, _P, _P]),
     "ddr_graph_structure": (C.c_int, [_P, _P, _P, _P, _P]),

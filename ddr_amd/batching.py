@@ -85,7 +85,7 @@ def collate_gauges(n_conus: int, subsets, gage_catchment=None) -> CollatedBatch:
     _lib.check(_lib.load().ddr_collate_gauges(int(n_conus), G, off.ctypes.data, rows.ctypes.data, cols.ctypes.data,
                                               gidx.ctypes.data, active.ctypes.data, C.byref(na), crow.ctypes.data,
                                               col.ctypes.data, C.byref(nnz), out_off.ctypes.data, out_idx.ctypes.data,
-                                              gage_c.ctypes.data))
+                                              len(out_idx), gage_c.ctypes.data))
     n = na.value
     outflow = [out_idx[out_off[g]:out_off[g + 1]].astype(np.int64) for g in range(G)]
     return CollatedBatch(int(n_conus), active[:n].astype(np.int64), crow[:n + 1].copy(), col[:nnz.value].astype(np.int64),

@@ -2,6 +2,7 @@
 // returned as ddr_status codes with a thread-local message (ddr_last_error).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -54,6 +55,10 @@ struct PendingStatus {
   unsigned* host = nullptr;  // pinned, kSlots x 4 words
   hipEvent_t ev[kSlots] = {};
   const char* what[kSlots] = {};
+  const void* graph[kSlots] = {};  // the launch's graph and stream, named in the error message
+  hipStream_t stream[kSlots] = {};
+  unsigned long long seq[kSlots] = {};
+  unsigned long long launches = 0;  // routing launches enqueued by this process
   int head = 0;
   bool failed = false;
   std::string msg;
@@ -62,9 +67,13 @@ struct PendingStatus {
     const unsigned* w = host + 4 * k;
     if (w[0] && !failed) {
       failed = true;
-      msg = std::to_string(w[0]) + " inter-workgroup hand-offs of a " + what[k] +
-            " launch timed out (first logical block " + std::to_string((int)w[1] - 1) +
-            "); its outputs hold NaN";
+      char id[96];
+      snprintf(id, sizeof(id), " (graph %p, stream %p, routing launch #%llu of this process)", graph[k],
+               (void*)stream[k], seq[k]);
+      msg = std::to_string(w[0]) + " inter-workgroup hand-offs of a " + what[k] + " launch" + id +
+            " timed out (first logical block " + std::to_string((int)w[1] - 1) +
+            "); its outputs hold NaN. Reported by the next library call: call ddr_status_check(1) at the "
+            "end of a run so that a timeout in the last launch is not missed";
     }
     (void)hipEventDestroy(ev[k]);
     ev[k] = nullptr;
@@ -82,7 +91,7 @@ struct PendingStatus {
     failed = false;
     return fail(DDR_ERR_TIMEOUT, msg);
   }
-  ddr_status enqueue(const void* status, hipStream_t s, const char* which) {
+  ddr_status enqueue(const void* status, hipStream_t s, const char* which, const void* g) {
     std::lock_guard<std::mutex> lk(mu);
     if (!host) DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&host), sizeof(unsigned) * 4 * kSlots, hipHostMallocDefault));
     const int k = head;
@@ -94,6 +103,9 @@ struct PendingStatus {
     DDR_HIP(hipMemcpyAsync(host + 4 * k, status, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, s));
     DDR_HIP(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
     what[k] = which;
+    graph[k] = g;
+    stream[k] = s;
+    seq[k] = ++launches;
     DDR_HIP(hipEventRecord(ev[k], s));
     return DDR_OK;
   }
@@ -211,7 +223,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   DDR_HIP(launch_route<R>(g, a, false, s));
   DDR_HIP(timing_mark(0, 1, s));
   // runoff (N, T) is written by the routing kernel itself (16-B row segments every 4 steps)
-  return g_pending.enqueue(status, s, "forward");
+  return g_pending.enqueue(status, s, "forward", gh);
 }
 
 template <typename R>
@@ -283,7 +295,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   DDR_HIP(launch_route<R>(g, a, true, s));
   DDR_HIP(timing_mark(1, 1, s));
   if (gqp) DDR_HIP(launch_scatter_qprime_grad<R>(g, a, qp_rows, gqp, s));
-  return g_pending.enqueue(status, s, "backward");
+  return g_pending.enqueue(status, s, "backward", gh);
 }
 
 template <typename R>
@@ -373,10 +385,10 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
 ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                               const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                               int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
-                              int32_t* gage_c) {
+                              int64_t out_idx_cap, int32_t* gage_c) {
   DDR_GUARD({
     return collate_gauges(n_conus, n_gauges, sub_off, rows, cols, gage_idx, active, n_active, crow, col, nnz,
-                          out_off, out_idx, gage_c);
+                          out_off, out_idx, out_idx_cap, gage_c);
   })
 }
 
@@ -510,7 +522,9 @@ ddr_status ddr_geometry_stats_f32(const float* q_daily, int64_t reach_stride, in
                                   const float* q_spatial, const float* slope, double depth_lb,
                                   double bottom_width_lb, float* out, void* stream) {
   DDR_GUARD({
-    if (n < 0 || days < 1 || days > 512) return fail(DDR_ERR_ARG, "geometry statistics: need 1 <= days <= 512");
+    // the long-window kernel sorts one variable of a reach in LDS: 4 B per day, the next power of two
+    if (n < 0 || days < 1 || days > kGeoLongMaxDays)
+      return fail(DDR_ERR_ARG, "geometry statistics: need 1 <= days <= " + std::to_string(kGeoLongMaxDays));
     if (n > 0 && (!q_daily || !n_manning || !p_spatial || !q_spatial || !slope || !out))
       return fail(DDR_ERR_ARG, "null geometry statistics argument");
     if (p_stride != 0 && p_stride != 1) return fail(DDR_ERR_ARG, "p_stride must be 0 or 1");

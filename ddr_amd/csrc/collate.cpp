@@ -22,7 +22,7 @@ namespace ddr {
 ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                           const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                           int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
-                          int32_t* gage_c) {
+                          int64_t out_idx_cap, int32_t* gage_c) {
   if (n_conus <= 0 || n_conus >= (int64_t(1) << 31) - 1) return fail(DDR_ERR_ARG, "bad CONUS size");
   if (n_gauges < 0 || !sub_off || (n_gauges > 0 && !gage_idx)) return fail(DDR_ERR_ARG, "bad gauge arrays");
   if (!active || !n_active || !crow || !nnz || !out_off || (n_gauges > 0 && (!out_idx || !gage_c)))
@@ -86,6 +86,9 @@ ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_
     gage_c[g] = x;
     const int64_t k0 = crow[x], k1 = crow[x + 1];
     int64_t o = out_off[g];
+    // several gauges on one reach each list its inflows: inconsistent subsets can exceed E + G entries
+    if (o + std::max<int64_t>(k1 - k0, 1) > out_idx_cap)
+      return fail(DDR_ERR_ARG, "outflow_idx lists exceed out_idx_cap (" + std::to_string(out_idx_cap) + " entries)");
     if (k1 > k0) {
       for (int64_t k = k0; k < k1; ++k) out_idx[o++] = col[k];
     } else {

@@ -12,6 +12,10 @@
 // step t of reach i runs at tick t + off(i) and every edge inside a workgroup has a slack of exactly
 // one tick ("as late as possible" wavefront).  Large basins are split into connected pieces whose
 // inter-piece edges become cut edges exchanged through global memory.
+//
+// The piece-level half (pack_pieces, finalize_blocks) is shared with the on-device builder
+// (devgraph.hip): both split the basins into the same pieces, number them the same way and hand the
+// same piece table to the same packer, so a device build emits the host build's schedule bit for bit.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -36,14 +40,6 @@ ddr_status upload(Graph* g, T** dst, const std::vector<T>& src) {
   *dst = static_cast<T*>(p);
   return DDR_OK;
 }
-
-struct Piece {
-  int64_t root;
-  int64_t size = 0;
-  int64_t height = 0;
-  int64_t dmax = 0;  // max in-piece dist including virtual inflows
-  int64_t xl = 0;    // confluence-list entries (reaches with more than two inflows, route.hip)
-};
 
 }  // namespace
 
@@ -76,6 +72,291 @@ ddr_status upload_schedule(Graph* g) {
   return DDR_OK;
 }
 
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- the packer's plan (capacity, generations) ------------------------------------------------
+ddr_status plan_init(int64_t n, int64_t bmax, const ddr_build_opts* opts, PackPlan& P) {
+  int dev = 0, n_cu = 0;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n_cu = prop.multiProcessorCount;
+  }
+  P.device = dev;
+  if (n_cu <= 0) n_cu = 256;
+  const int bs = kBlockThreads;
+  P.n = n;
+  P.hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, kDefaultBlockReaches);
+  if (opts && opts->max_block_reaches > 0) P.hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, opts->max_block_reaches);
+  P.target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu) * kBlocksPerCU;
+  P.resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
+  // Capacity floor: one wave-slice per SIMD (4 x 64 reaches).  A tick costs ~0.66 us + 0.49 us per
+  // slice on the busiest SIMD (DESIGN.md section 4), so a light load (n well below 256 x 1024) is
+  // cheapest spread thin over many workgroups, not packed into a few full ones.
+  P.min_cap = std::min<int64_t>(kMinBlockCap, bs);
+  P.cap = std::min<int64_t>(P.hard_cap, std::max<int64_t>(P.min_cap, (n + P.target - 1) / P.target));
+  // ... rounded up to whole slices per SIMD (4 x 64 reaches) at light and medium loads: a tick costs
+  // per slice on the busiest SIMD, so the rounding keeps that cost and makes fewer, larger pieces --
+  // fewer cut edges and shorter block chains (routing of a C3 8-way shard 8.1 -> 7.2 ms, of C5's
+  // giant-basin shard 57.6 -> 54.3 ms); at full load (C3, C5 on one GPU) it measured slower
+  // (profiles/r02/ab_defer_early.txt)
+#ifndef DDR_CAP_QUANT
+#define DDR_CAP_QUANT 256
+#endif
+#ifndef DDR_CAP_QUANT_MAX
+#define DDR_CAP_QUANT_MAX 2048
+#endif
+  if (DDR_CAP_QUANT > 1 && P.cap <= DDR_CAP_QUANT_MAX)
+    P.cap = std::min<int64_t>(P.hard_cap, (P.cap + DDR_CAP_QUANT - 1) / DDR_CAP_QUANT * DDR_CAP_QUANT);
+  P.cap_start = P.cap;
+  P.steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
+  // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
+  P.fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
+  // block capacity rounded down to a multiple of this many reaches (a tick costs per 256-reach
+  // slice-per-SIMD unit; experiments: DDR_PACK_QUANT)
+  P.pack_quant = getenv("DDR_PACK_QUANT") ? atol(getenv("DDR_PACK_QUANT")) : 1;
+  // Split threshold (pieces up to scap_pct % of the capacity): with a dominant basin (C4/C5: 0.35 N)
+  // its chain of pieces is the critical path, and pieces at 80 % leave the packer room to give chain
+  // blocks fewer reaches; without one (C3: 256 basins of at most 2 % of N) pieces at the full
+  // capacity mean fewer cut edges (C3 38.7 -> 36.5 ms per step; C5 at 100 %: 138 -> 149 ms;
+  // profiles/r02/ab_defer_early.txt)
+  P.scap_pct = bmax * 10 < n ? 100 : 80;
+#ifdef DDR_SCAP_PCT
+  P.scap_pct = DDR_SCAP_PCT;
+#endif
+  P.weighted = true;
+  P.gen = 1;
+  P.dbg = getenv("DDR_DEBUG_PART") != nullptr;
+  return DDR_OK;
+}
+
+// ---- packing of the pieces into workgroups ----------------------------------------------------
+// Workgroups take their logical block index from a ticket counter in block order (route.hip:
+// take_ticket), and blocks are numbered by piece height, so a running workgroup's producers are
+// running or done: a schedule with more blocks than resident workgroups is still deadlock-free.
+// The packer first tries to fit one resident generation (all blocks co-resident, fully time-
+// pipelined): path-weighted packing, then unweighted; failing both it packs gen x resident
+// smaller blocks (every extra generation costs about T more ticks of the blocks it holds).
+ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* outcome) {
+  const size_t np = pt.count();
+  // virtual inflows deepen the consuming piece by one tick; piece heights (children first: a child
+  // piece is numbered after its parent)
+  std::vector<int64_t> dmax(pt.dmax), height(np, 0);
+  for (int64_t p = (int64_t)np - 1; p >= 0; --p) {
+    const int64_t q = pt.parent[p];
+    if (q >= 0) {
+      dmax[q] = std::max<int64_t>(dmax[q], pt.dloc_down[p] + 1);
+      height[q] = std::max(height[q], height[p] + 1);
+    }
+  }
+  int64_t ncut = 0;
+  for (size_t p = 0; p < np; ++p) ncut += (pt.parent[p] >= 0);
+  // Packing: pieces of equal height share blocks (so the block dependency graph is a DAG),
+  // worst-fit by weight.  The blocks of a split basin progress at the pace of their slowest
+  // member (a consumer waits for its producers, forward and backward alike), so every block
+  // holding a piece of a long path needs T + (path length) ticks, not T + dmax: a piece is
+  // weighted by (T + L) / T with L the longest source-to-outlet path through its root, plus one
+  // chunk per inter-block hop on it.  Chain blocks get fewer reaches and tick faster (a tick
+  // costs in proportion to the reaches of a workgroup).
+  std::vector<int64_t> hops_down(np, 0);
+  for (size_t p = 0; p < np; ++p)  // parents before children (numbering order)
+    if (pt.parent[p] >= 0) hops_down[p] = hops_down[pt.parent[p]] + 1;
+  std::vector<double> fac(np);
+  double wsum = 0.0;
+  for (size_t p = 0; p < np; ++p) {
+    const double L = (double)(pt.ht_root[p] + pt.dist_root[p] + kChunk * (hops_down[p] + height[p]));
+    fac[p] = P.weighted ? std::pow((P.steps + L) / P.steps, P.fac_pow) : 1.0;
+  }
+  for (size_t p = 0; p < np; ++p) wsum += (double)pt.size[p] * fac[p];
+  // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
+  // Pieces are taken by factor (descending) so blocks gather pieces of similar factor; capw is
+  // the smallest (1 % steps) that packs into the target number of workgroups.
+  std::vector<int64_t> order(np), block_of_piece(np), load;
+  std::vector<double> bcap;
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+    if (height[a] != height[b]) return height[a] < height[b];
+    if (fac[a] != fac[b]) return fac[a] > fac[b];
+    return pt.size[a] > pt.size[b];
+  });
+  const int64_t limit = ncut > 0 ? std::min<int64_t>(P.target, P.resident) * P.gen : P.target;
+  // capw_k = capw_0 * 1.01^k; beyond k_sat (capw / fac >= hard_cap for every piece) the packing no
+  // longer changes.  The block count falls with k, so the smallest k that fits is binary-searched
+  // (a handful of packing passes instead of one per 1 % step).
+  double maxfac = 1.0;
+  for (double f : fac) maxfac = std::max(maxfac, f);
+  const double capw0 = wsum / (double)limit;
+  auto pack = [&](int k) {
+    const double capw = capw0 * std::pow(1.01, (double)k);
+    load.clear();
+    bcap.clear();
+    size_t hstart = 0;  // first block of the current height class
+    int64_t curh = -1;
+    for (int64_t p : order) {
+      if (height[p] != curh) {
+        curh = height[p];
+        hstart = load.size();
+      }
+      int64_t best = -1;
+      const int64_t sz = pt.size[p];
+      for (size_t b = hstart; b < load.size(); ++b)
+        if ((double)(load[b] + sz) <= bcap[b] && (best < 0 || load[b] < load[best])) best = (int64_t)b;
+      if (best < 0) {
+        best = (int64_t)load.size();
+        load.push_back(0);
+        double bc = std::min<double>((double)P.hard_cap, std::max<double>((double)sz, capw / fac[p]));
+        if (P.pack_quant > 1 && bc >= (double)P.pack_quant)
+          bc = std::max<double>((double)sz, std::floor(bc / (double)P.pack_quant) * (double)P.pack_quant);
+        bcap.push_back(bc);
+      }
+      load[best] += sz;
+      block_of_piece[p] = best;
+    }
+    return (int64_t)load.size();
+  };
+  const int k_sat = std::max(0, (int)std::ceil(std::log((double)P.hard_cap * maxfac / capw0) / std::log(1.01)));
+  int npass = 1;
+  if (pack(0) > limit) {
+    int lo = 0, hi = k_sat;  // pack(lo) > limit; find the smallest k in (lo, hi] with pack(k) <= limit
+    ++npass;
+    if (pack(hi) <= limit) {
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) / 2;
+        ++npass;
+        if (pack(mid) <= limit) hi = mid;
+        else lo = mid;
+      }
+      ++npass;
+      pack(hi);
+    }
+  }
+  const int64_t nblocks = (int64_t)load.size();
+  if (P.dbg) {
+    fprintf(stderr, "[part] pack passes %d\n", npass);
+    fprintf(stderr, "[part] cap %ld hard %ld gen %ld weighted %d pieces %zu blocks %ld cut %ld\n", (long)P.cap,
+            (long)P.hard_cap, (long)P.gen, (int)P.weighted, np, (long)nblocks, (long)ncut);
+  }
+  // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if a workgroup
+  // would no longer fit on a CU
+  std::vector<int64_t> bv(nblocks, 0), bc(nblocks, 0), bx(nblocks, 0);
+  for (size_t p = 0; p < np; ++p) {
+    bx[block_of_piece[p]] += pt.xl[p];
+    if (pt.parent[p] >= 0) {
+      bv[block_of_piece[pt.parent[p]]]++;
+      bc[block_of_piece[p]]++;
+    }
+  }
+  int64_t ms = 0, mv = 0, mc = 0, mx = 0;
+  for (int64_t b = 0; b < nblocks; ++b) {
+    ms = std::max(ms, load[b] + bv[b]);
+    mv = std::max(mv, bv[b]);
+    mc = std::max(mc, bc[b]);
+    mx = std::max(mx, bx[b]);
+  }
+  const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4),
+                               route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
+  if (P.dbg) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
+  // (a count failure at the capacity ceiling of the unweighted packing goes to more generations:
+  // shrinking the capacity for LDS would only add blocks)
+  const bool count_dead = ncut > 0 && nblocks > limit && P.cap >= P.hard_cap && !P.weighted;
+  if (!count_dead && (need > kLdsBudget || mx >= kMaxConfluenceList)) {
+    if (P.hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
+    P.hard_cap -= std::max<int64_t>(1, P.hard_cap / 32);
+    P.cap = std::min(P.cap, P.hard_cap);
+    *outcome = kPackResplit;
+    return DDR_OK;
+  }
+  if (ncut > 0 && nblocks > limit) {
+    *outcome = kPackResplit;
+    if (P.cap < P.hard_cap) {
+      P.cap = std::min<int64_t>(P.hard_cap, P.cap + P.cap / 32 + 1);
+      return DDR_OK;
+    }
+    if (P.weighted) {
+      P.weighted = false;
+      P.cap = P.cap_start;
+      return DDR_OK;
+    }
+    if (++P.gen > 64) return fail(DDR_ERR_CAPACITY, "graph cannot be packed into workgroups");
+    P.weighted = true;
+    const int64_t per_gen = std::min<int64_t>(P.target, P.resident) * P.gen;
+    P.cap = std::min<int64_t>(P.hard_cap, std::max<int64_t>(P.min_cap, (P.n + per_gen - 1) / per_gen));
+    return DDR_OK;
+  }
+  *outcome = kPackDone;
+  R.nblocks = nblocks;
+  R.ncut = ncut;
+  R.block_of_piece = std::move(block_of_piece);
+  R.load = std::move(load);
+  R.bv = std::move(bv);
+  R.bc = std::move(bc);
+  R.bx = std::move(bx);
+  R.bdmax.assign(nblocks, 0);
+  for (size_t p = 0; p < np; ++p) R.bdmax[R.block_of_piece[p]] = std::max(R.bdmax[R.block_of_piece[p]], dmax[p]);
+  return DDR_OK;
+}
+
+// Block descriptors and the graph-wide sizes from the packing (counts only: the per-reach arrays are
+// emitted by the host or the device builder in the same order -- blocks contiguous, inside a block by
+// (tick offset, reference index); a block's cut edges, virtual inflows and confluence lists in that
+// position order).
+ddr_status finalize_blocks(Graph* g, const PackPlan& P, const PackResult& R) {
+  const int64_t nb = R.nblocks;
+  g->generations = P.gen;
+  g->resident = P.resident;
+  g->n_cut = R.ncut;
+  g->blocks.assign(nb, BlockDesc{});
+  int64_t p0 = 0, pre_dn = 0, v0 = 0, c0 = 0, x0 = 0, max_load = 0;
+  g->max_slots = g->max_virt = g->max_cout = g->max_xl = 0;
+  g->max_block_depth = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    BlockDesc& B = g->blocks[b];
+    B.pos0 = (int32_t)p0;
+    B.nloc = (int32_t)R.load[b];
+    B.virt0 = (int32_t)v0;
+    B.nvirt = (int32_t)R.bv[b];
+    B.cout0 = (int32_t)c0;
+    B.ncout = (int32_t)R.bc[b];
+    B.dmax = (int32_t)R.bdmax[b];
+    B.nxl = (int32_t)R.bx[b];
+    B.pre_dn = pre_dn;
+    B.xl0 = (int32_t)x0;
+    B.pad = 0;
+    g->max_xl = std::max<int>(g->max_xl, B.nxl);
+    g->max_slots = std::max<int>(g->max_slots, B.nloc + B.nvirt);
+    g->max_virt = std::max<int>(g->max_virt, B.nvirt);
+    g->max_cout = std::max<int>(g->max_cout, B.ncout);
+    g->max_block_depth = std::max<int64_t>(g->max_block_depth, B.dmax + 1);
+    max_load = std::max<int64_t>(max_load, R.load[b]);
+    pre_dn += R.bdmax[b] * R.load[b];
+    p0 += R.load[b];
+    v0 += R.bv[b];
+    c0 += R.bc[b];
+    x0 += R.bx[b];
+  }
+  g->sum_dn = pre_dn;
+  g->max_nloc = (int)max_load;
+  g->n_xlist = x0;
+  int kr = 1;
+  while (int64_t(kr) * kBlockThreads < max_load) kr *= 2;
+  g->kr = kr;
+  if (g->max_virt > kBlockThreads || g->max_cout > kBlockThreads)
+    return fail(DDR_ERR_CAPACITY, "too many inter-workgroup edges in one workgroup");
+  return DDR_OK;
+}
+
+// FNV-1a over the schedule arrays (DDR_DEBUG_PART): the host and device builds print it.
+unsigned long long schedule_fingerprint(const HostSchedule& H) {
+  unsigned long long h = 1469598103934665603ull;
+  auto mix = [&](const std::vector<int32_t>& v) {
+    for (int32_t x : v) h = (h ^ (unsigned)x) * 1099511628211ull;
+  };
+  mix(H.ref); mix(H.off); mix(H.upb); mix(H.upc); mix(H.dloc); mix(H.cut); mix(H.xoff); mix(H.uplist); mix(H.xlist);
+  mix(H.v_edge); mix(H.v_off); mix(H.v_dloc); mix(H.cout_loc);
+  return h;
+}
+
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out) {
   if (n <= 0) return fail(DDR_ERR_ARG, "graph must have at least one reach");
@@ -84,11 +365,10 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   auto g = std::make_unique<Graph>();
   g->n = n;
   const bool dbg = getenv("DDR_DEBUG_PART") != nullptr;
-  auto tnow = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  double tp = tnow();
+  double tp = now_ms();
   auto phase = [&](const char* what) {
     if (!dbg) return;
-    const double t = tnow();
+    const double t = now_ms();
     fprintf(stderr, "[part] %-10s %8.2f ms\n", what, t - tp);
     tp = t;
   };
@@ -138,44 +418,6 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   for (int64_t i = 0; i < n; ++i) g->n_basins += (g->down[i] < 0);
   phase("csr+tree");
 
-  // ---- partition: split basins larger than cap into connected pieces ---------------------
-  int dev = 0, n_cu = 0, resident = 0;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n_cu = prop.multiProcessorCount;
-  }
-  g->device = dev;
-  if (n_cu <= 0) n_cu = 256;
-  const int bs = kBlockThreads;
-  int64_t hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, kDefaultBlockReaches);
-  if (opts && opts->max_block_reaches > 0) hard_cap = std::min<int64_t>(int64_t(bs) * kMaxKR, opts->max_block_reaches);
-  int64_t target = (opts && opts->target_blocks > 0) ? opts->target_blocks : int64_t(n_cu) * kBlocksPerCU;
-  resident = (opts && opts->max_resident > 0) ? opts->max_resident : n_cu * kBlocksPerCU;
-  // Capacity floor: one wave-slice per SIMD (4 x 64 reaches).  A tick costs ~0.66 us + 0.49 us per
-  // slice on the busiest SIMD (DESIGN.md section 4), so a light load (n well below 256 x 1024) is
-  // cheapest spread thin over many workgroups, not packed into a few full ones.
-  const int64_t min_cap = std::min<int64_t>(kMinBlockCap, bs);
-  int64_t cap = std::min<int64_t>(hard_cap, std::max<int64_t>(min_cap, (n + target - 1) / target));
-  // ... rounded up to whole slices per SIMD (4 x 64 reaches) at light and medium loads: a tick costs
-  // per slice on the busiest SIMD, so the rounding keeps that cost and makes fewer, larger pieces --
-  // fewer cut edges and shorter block chains (routing of a C3 8-way shard 8.1 -> 7.2 ms, of C5's
-  // giant-basin shard 57.6 -> 54.3 ms); at full load (C3, C5 on one GPU) it measured slower
-  // (profiles/r02/ab_defer_early.txt)
-#ifndef DDR_CAP_QUANT
-#define DDR_CAP_QUANT 256
-#endif
-#ifndef DDR_CAP_QUANT_MAX
-#define DDR_CAP_QUANT_MAX 2048
-#endif
-  if (DDR_CAP_QUANT > 1 && cap <= DDR_CAP_QUANT_MAX)
-    cap = std::min<int64_t>(hard_cap, (cap + DDR_CAP_QUANT - 1) / DDR_CAP_QUANT * DDR_CAP_QUANT);
-  const double steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
-  // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
-  const double fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
-  // block capacity rounded down to a multiple of this many reaches (a tick costs per 256-reach
-  // slice-per-SIMD unit; experiments: DDR_PACK_QUANT)
-  const int64_t pack_quant = getenv("DDR_PACK_QUANT") ? atol(getenv("DDR_PACK_QUANT")) : 1;
-
   // Splitting works on full-subtree sizes and heights: sub(i) = reaches draining through i,
   // ht(i) = longest path from i up to a source.
   std::vector<int32_t> sub(n, 1), ht(n, 0);
@@ -184,34 +426,20 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       sub[i] += sub[col[k]];
       ht[i] = std::max(ht[i], ht[col[k]] + 1);
     }
-  std::vector<int32_t> piece(n), resid(n), stem(n), dloc_piece(n);
-  std::vector<char> is_root(n);
-  std::vector<Piece> pieces;
-  std::vector<int64_t> others;
-  // Workgroups take their logical block index from a ticket counter in block order (route.hip:
-  // take_ticket), and blocks are numbered by piece height, so a running workgroup's producers are
-  // running or done: a schedule with more blocks than resident workgroups is still deadlock-free.
-  // The packer first tries to fit one resident generation (all blocks co-resident, fully time-
-  // pipelined): path-weighted packing, then unweighted; failing both it packs gen x resident
-  // smaller blocks (every extra generation costs about T more ticks of the blocks it holds).
-  // Split threshold (pieces up to scap_pct % of the capacity): with a dominant basin (C4/C5: 0.35 N)
-  // its chain of pieces is the critical path, and pieces at 80 % leave the packer room to give chain
-  // blocks fewer reaches; without one (C3: 256 basins of at most 2 % of N) pieces at the full
-  // capacity mean fewer cut edges (C3 38.7 -> 36.5 ms per step; C5 at 100 %: 138 -> 149 ms;
-  // profiles/r02/ab_defer_early.txt)
-  int64_t scap_pct = 80;
+  int64_t bmax = 0;
   {
     std::vector<int32_t> bsz(n, 0);
-    int64_t bmax = 0;
     for (int64_t i = 0; i < n; ++i) bmax = std::max<int64_t>(bmax, ++bsz[g->basin[i]]);
-    if (bmax * 10 < n) scap_pct = 100;
-#ifdef DDR_SCAP_PCT
-    scap_pct = DDR_SCAP_PCT;
-#endif
   }
-  bool weighted = true;
-  int64_t gen = 1;
-  const int64_t cap_start = cap;
+  PackPlan plan;
+  ddr_status st = plan_init(n, bmax, opts, plan);
+  if (st) return st;
+  g->device = plan.device;
+  std::vector<int32_t> piece(n), resid(n), stem(n), dloc_piece(n);
+  std::vector<char> is_root(n);
+  std::vector<int64_t> others;
+  PieceTable pt;
+  PackResult pr;
   for (;;) {
     // Stem-preserving split (bottom-up).  A reach whose subtree exceeds the capacity keeps its
     // deepest child (the main stem: every block boundary crossed along the longest flow path adds
@@ -220,7 +448,7 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
     // least lseg reaches.  The stem child is cut only when the piece is full.
     // Pieces of split basins are kept below the block capacity: they land in blocks on long
     // chains, whose packing weight is up to ~(T + depth) / T times their size.
-    const int64_t scap = cap * scap_pct / 100;
+    const int64_t scap = plan.scap();
     const int64_t lseg = scap / 8;
     std::fill(is_root.begin(), is_root.end(), 0);
     for (int64_t i = 0; i < n; ++i) {
@@ -254,352 +482,154 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
       resid[i] = base + acc;
       stem[i] = keep ? 1 + stem[dc] : 1;
     }
-    pieces.clear();
+    // pieces numbered by descending root index (a child piece after its parent)
+    pt = PieceTable{};
     for (int64_t i = n - 1; i >= 0; --i) {
       int64_t d = g->down[i];
       if (d < 0 || is_root[i]) {
         is_root[i] = 1;
-        piece[i] = (int64_t)pieces.size();
-        pieces.push_back(Piece{i});
+        piece[i] = (int32_t)pt.count();
+        pt.root.push_back(i);
+        pt.size.push_back(0);
+        pt.dmax.push_back(0);
+        pt.xl.push_back(0);
+        pt.parent.push_back(d < 0 ? -1 : piece[d]);
+        pt.dloc_down.push_back(d < 0 ? 0 : dloc_piece[d]);
+        pt.ht_root.push_back(ht[i]);
+        pt.dist_root.push_back(g->dist[i]);
         dloc_piece[i] = 0;
       } else {
         piece[i] = piece[d];
         dloc_piece[i] = dloc_piece[d] + 1;
       }
-      Piece& P = pieces[piece[i]];
-      P.size++;
-      if (cnt[i + 1] - cnt[i] > 2) P.xl += cnt[i + 1] - cnt[i];
-      P.dmax = std::max<int64_t>(P.dmax, dloc_piece[i]);
-    }
-    // virtual inflows deepen the consuming piece by one tick; piece heights (children first:
-    // a child piece is created after its parent in the loop above)
-    for (int64_t p = (int64_t)pieces.size() - 1; p >= 0; --p) {
-      int64_t r = pieces[p].root, d = g->down[r];
-      if (d >= 0) {
-        Piece& Q = pieces[piece[d]];
-        Q.dmax = std::max<int64_t>(Q.dmax, dloc_piece[d] + 1);
-        Q.height = std::max(Q.height, pieces[p].height + 1);
-      }
+      const int64_t p = piece[i];
+      pt.size[p]++;
+      if (cnt[i + 1] - cnt[i] > 2) pt.xl[p] += cnt[i + 1] - cnt[i];
+      pt.dmax[p] = std::max<int64_t>(pt.dmax[p], dloc_piece[i]);
     }
     phase("split");
-    int64_t ncut = 0;
-    for (auto& P : pieces) ncut += (g->down[P.root] >= 0);
-    // Packing: pieces of equal height share blocks (so the block dependency graph is a DAG),
-    // worst-fit by weight.  The blocks of a split basin progress at the pace of their slowest
-    // member (a consumer waits for its producers, forward and backward alike), so every block
-    // holding a piece of a long path needs T + (path length) ticks, not T + dmax: a piece is
-    // weighted by (T + L) / T with L the longest source-to-outlet path through its root, plus one
-    // chunk per inter-block hop on it.  Chain blocks get fewer reaches and tick faster (a tick
-    // costs in proportion to the reaches of a workgroup).
-    std::vector<int64_t> hops_down(pieces.size(), 0);
-    for (size_t p = 0; p < pieces.size(); ++p) {  // parents before children (creation order)
-      const int64_t d = g->down[pieces[p].root];
-      if (d >= 0) hops_down[p] = hops_down[piece[d]] + 1;
-    }
-    std::vector<double> fac(pieces.size());
-    double wsum = 0.0;
-    for (size_t p = 0; p < pieces.size(); ++p) {
-      const int64_t r = pieces[p].root;
-      const double L = (double)(ht[r] + g->dist[r] + kChunk * (hops_down[p] + pieces[p].height));
-      fac[p] = weighted ? std::pow((steps + L) / steps, fac_pow) : 1.0;
-    }
-    for (size_t p = 0; p < pieces.size(); ++p) wsum += (double)pieces[p].size * fac[p];
-    // A block's tick budget is set by its most constrained piece: capacity capw / max factor.
-    // Pieces are taken by factor (descending) so blocks gather pieces of similar factor; capw is
-    // the smallest (1 % steps) that packs into the target number of workgroups.
-    std::vector<int64_t> order(pieces.size()), block_of_piece(pieces.size()), load;
-    std::vector<double> bcap;
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
-      if (pieces[a].height != pieces[b].height) return pieces[a].height < pieces[b].height;
-      if (fac[a] != fac[b]) return fac[a] > fac[b];
-      return pieces[a].size > pieces[b].size;
-    });
-    int64_t ncut0 = 0;
-    for (auto& P : pieces) ncut0 += (g->down[P.root] >= 0);
-    const int64_t limit = ncut0 > 0 ? std::min<int64_t>(target, resident) * gen : target;
-    // capw_k = capw_0 * 1.01^k; beyond k_sat (capw / fac >= hard_cap for every piece) the packing no
-    // longer changes.  The block count falls with k, so the smallest k that fits is binary-searched
-    // (a handful of packing passes instead of one per 1 % step).
-    double maxfac = 1.0;
-    for (double f : fac) maxfac = std::max(maxfac, f);
-    const double capw0 = wsum / (double)limit;
-    auto pack = [&](int k) {
-      const double capw = capw0 * std::pow(1.01, (double)k);
-      load.clear();
-      bcap.clear();
-      size_t hstart = 0;  // first block of the current height class
-      int64_t curh = -1;
-      for (int64_t p : order) {
-        if (pieces[p].height != curh) {
-          curh = pieces[p].height;
-          hstart = load.size();
-        }
-        int64_t best = -1;
-        const int64_t sz = pieces[p].size;
-        for (size_t b = hstart; b < load.size(); ++b)
-          if ((double)(load[b] + sz) <= bcap[b] && (best < 0 || load[b] < load[best])) best = (int64_t)b;
-        if (best < 0) {
-          best = (int64_t)load.size();
-          load.push_back(0);
-          double bc = std::min<double>((double)hard_cap, std::max<double>((double)sz, capw / fac[p]));
-          if (pack_quant > 1 && bc >= (double)pack_quant)
-            bc = std::max<double>((double)sz, std::floor(bc / (double)pack_quant) * (double)pack_quant);
-          bcap.push_back(bc);
-        }
-        load[best] += sz;
-        block_of_piece[p] = best;
-      }
-      return (int64_t)load.size();
-    };
-    const int k_sat = std::max(0, (int)std::ceil(std::log((double)hard_cap * maxfac / capw0) / std::log(1.01)));
-    int npass = 1;
-    if (pack(0) > limit) {
-      int lo = 0, hi = k_sat;  // pack(lo) > limit; find the smallest k in (lo, hi] with pack(k) <= limit
-      ++npass;
-      if (pack(hi) <= limit) {
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) / 2;
-          ++npass;
-          if (pack(mid) <= limit) hi = mid;
-          else lo = mid;
-        }
-        ++npass;
-        pack(hi);
-      }
-    }
-    const int64_t nblocks = (int64_t)load.size();
-    if (dbg) fprintf(stderr, "[part] pack passes %d\n", npass);
+    int outcome = kPackDone;
+    if ((st = pack_pieces(plan, pt, pr, &outcome))) return st;
     phase("pack");
-    if (getenv("DDR_DEBUG_PART"))
-      fprintf(stderr, "[part] cap %ld hard %ld gen %ld weighted %d pieces %zu blocks %ld cut %ld\n", (long)cap,
-              (long)hard_cap, (long)gen, (int)weighted, pieces.size(), (long)nblocks, (long)ncut);
-    {
-      // LDS of the fp32 kernels at the resulting slot / ring sizes; shrink the capacity if two
-      // workgroups would no longer fit on a CU
-      std::vector<int64_t> bv(nblocks, 0), bc(nblocks, 0), bx(nblocks, 0);
-      for (size_t p = 0; p < pieces.size(); ++p) {
-        bx[block_of_piece[p]] += pieces[p].xl;
-        const int64_t d = g->down[pieces[p].root];
-        if (d >= 0) {
-          bv[block_of_piece[piece[d]]]++;
-          bc[block_of_piece[p]]++;
-        }
-      }
-      int64_t ms = 0, mv = 0, mc = 0, mx = 0;
-      for (int64_t b = 0; b < nblocks; ++b) {
-        ms = std::max(ms, load[b] + bv[b]);
-        mv = std::max(mv, bv[b]);
-        mc = std::max(mc, bc[b]);
-        mx = std::max(mx, bx[b]);
-      }
-      const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4),
-                                   route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
-      if (getenv("DDR_DEBUG_PART"))
-        fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
-      // (a count failure at the capacity ceiling of the unweighted packing goes to more generations:
-      // shrinking the capacity for LDS would only add blocks)
-      const bool count_dead = ncut > 0 && nblocks > limit && cap >= hard_cap && !weighted;
-      if (!count_dead && (need > kLdsBudget || mx >= kMaxConfluenceList)) {
-        if (hard_cap <= 64) return fail(DDR_ERR_CAPACITY, "workgroup LDS budget exceeded");
-        hard_cap -= std::max<int64_t>(1, hard_cap / 32);
-        cap = std::min(cap, hard_cap);
-        continue;
-      }
-    }
-    if (ncut > 0 && nblocks > limit) {
-      if (cap < hard_cap) {
-        cap = std::min<int64_t>(hard_cap, cap + cap / 32 + 1);
-        continue;
-      }
-      if (weighted) {
-        weighted = false;
-        cap = cap_start;
-        continue;
-      }
-      if (++gen > 64) return fail(DDR_ERR_CAPACITY, "graph cannot be packed into workgroups");
-      weighted = true;
-      const int64_t per_gen = std::min<int64_t>(target, resident) * gen;
-      cap = std::min<int64_t>(hard_cap, std::max<int64_t>(min_cap, (n + per_gen - 1) / per_gen));
-      continue;
-    }
-    phase("lds");
-    g->generations = gen;
-    g->resident = resident;
-    // ---- emit the schedule ---------------------------------------------------------------
-    g->n_pieces = (int64_t)pieces.size();
-    g->n_cut = ncut;
-    g->block_of.assign(n, 0);
-    for (int64_t i = 0; i < n; ++i) g->block_of[i] = block_of_piece[piece[i]];
-    std::vector<int64_t> bdmax(nblocks, 0);
-    for (size_t p = 0; p < pieces.size(); ++p)
-      bdmax[block_of_piece[p]] = std::max(bdmax[block_of_piece[p]], pieces[p].dmax);
-    std::vector<int32_t> offv(n);
-    for (int64_t i = 0; i < n; ++i) offv[i] = bdmax[g->block_of[i]] - dloc_piece[i];
-    // internal order (block, tick offset, reference index): two stable counting sorts over the
-    // ascending reach ids, by offset and then by block (O(n), no comparison sort)
-    std::vector<int64_t> bstart(nblocks + 1, 0);
-    std::vector<int32_t> order_all(n);
-    {
-      int64_t omax = 0;
-      for (int64_t b = 0; b < nblocks; ++b) omax = std::max(omax, bdmax[b]);
-      std::vector<int64_t> oc(omax + 2, 0);
-      for (int64_t i = 0; i < n; ++i) oc[offv[i] + 1]++;
-      for (int64_t o = 0; o <= omax; ++o) oc[o + 1] += oc[o];
-      std::vector<int32_t> by_off(n);
-      for (int64_t i = 0; i < n; ++i) by_off[oc[offv[i]]++] = (int32_t)i;
-      for (int64_t i = 0; i < n; ++i) bstart[g->block_of[i] + 1]++;
-      for (int64_t b = 0; b < nblocks; ++b) bstart[b + 1] += bstart[b];
-      std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
-      for (int64_t j = 0; j < n; ++j) {
-        const int32_t i = by_off[j];
-        order_all[fillb[g->block_of[i]]++] = i;
-      }
-    }
-    struct Span {
-      const int32_t* b;
-      const int32_t* e;
-      const int32_t* begin() const { return b; }
-      const int32_t* end() const { return e; }
-      size_t size() const { return (size_t)(e - b); }
-      int64_t operator[](size_t k) const { return b[k]; }
-    };
-    auto members_of = [&](int64_t b) { return Span{order_all.data() + bstart[b], order_all.data() + bstart[b + 1]}; };
-    phase("members");
-    // internal order: blocks contiguous; inside a block by (tick offset, reference index)
-    std::vector<int32_t> pos(n), local(n);
-    HostSchedule& H = g->hs;
-    H = HostSchedule{};
-    std::vector<int32_t>&ref = H.ref, &offs = H.off, &upb = H.upb, &upc = H.upc, &dl = H.dloc, &cut = H.cut,
-                        &xoff = H.xoff, &uplist = H.uplist, &xlist = H.xlist, &v_edge = H.v_edge, &v_off = H.v_off,
-                        &v_dloc = H.v_dloc, &cout_loc = H.cout_loc;
-    ref.resize(n);
-    offs.resize(n);
-    upb.resize(n);
-    upc.resize(n);
-    dl.resize(n);
-    cut.assign(n, -1);
-    xoff.assign(n, -1);
-    std::vector<int32_t> edge_id(n, -1);
-    // Cut edges are numbered in (block, local position) order, i.e. by their index in cout_loc: the
-    // forward kernel derives a cut reach's granule row from B.cout0 + its rank among the block's
-    // cut reaches (route.hip), with no table load in the tick.
-    phase("sort");
-    int64_t eid = 0;
-    for (int64_t b = 0; b < nblocks; ++b)
-      for (int64_t i : members_of(b))
-        if (g->down[i] >= 0 && g->block_of[g->down[i]] != b) edge_id[i] = eid++;
-    g->n_cut = eid;  // inter-workgroup edges (pieces packed into one block hand off in LDS)
-    g->blocks.assign(nblocks, BlockDesc{});
-    int64_t p0 = 0, pre_dn = 0;
-    g->max_slots = g->max_virt = g->max_cout = g->max_xl = 0;
-    g->max_block_depth = 0;
-    int64_t max_load = 0;
-    for (int64_t b = 0; b < nblocks; ++b) {
-      const Span m = members_of(b);
-      for (size_t r = 0; r < m.size(); ++r) {
-        pos[m[r]] = p0 + (int64_t)r;
-        local[m[r]] = (int64_t)r;
-      }
-      BlockDesc& B = g->blocks[b];
-      B.pos0 = (int32_t)p0;
-      B.nloc = (int32_t)m.size();
-      B.virt0 = (int32_t)v_edge.size();
-      B.cout0 = (int32_t)cout_loc.size();
-      B.dmax = (int32_t)bdmax[b];
-      B.pre_dn = pre_dn;
-      B.xl0 = (int32_t)xlist.size();
-      max_load = std::max<int64_t>(max_load, (int64_t)m.size());
-      for (size_t r = 0; r < m.size(); ++r) {
-        int64_t i = m[r];
-        int64_t P = p0 + (int64_t)r;
-        ref[P] = (int32_t)i;
-        offs[P] = (int32_t)offv[i];
-        upb[P] = (int32_t)uplist.size();
-        upc[P] = (int32_t)(cnt[i + 1] - cnt[i]);
-        for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
-          int64_t j = col[k];
-          if (g->block_of[j] == b) {
-            uplist.push_back((int32_t)local[j]);
-          } else {
-            // virtual inflow of cut edge j -> i
-            uplist.push_back((int32_t)(m.size() + (v_edge.size() - B.virt0)));
-            v_edge.push_back((int32_t)edge_id[j]);
-            v_off.push_back((int32_t)(offv[i] - 1));
-            v_dloc.push_back((int32_t)r);
-          }
-        }
-        if (upc[P] > 2) {
-          // confluence list: [c, u1, ..., u_{c-1}] at xoff (block-local), see route.hip pack_up
-          xoff[P] = (int32_t)(xlist.size() - B.xl0);
-          xlist.push_back(upc[P]);
-          for (int32_t k = 1; k < upc[P]; ++k) xlist.push_back(uplist[upb[P] + k]);
-        }
-        int64_t d = g->down[i];
-        dl[P] = (d >= 0 && g->block_of[d] == b) ? -2 : -1;  // resolved below (local of d)
-        if (d >= 0 && g->block_of[d] != b) {
-          cut[P] = (int32_t)edge_id[i];
-          cout_loc.push_back((int32_t)r);
-        }
-      }
-      B.nvirt = (int32_t)(v_edge.size() - B.virt0);
-      B.ncout = (int32_t)(cout_loc.size() - B.cout0);
-      B.nxl = (int32_t)(xlist.size() - B.xl0);
-      g->max_xl = std::max<int>(g->max_xl, B.nxl);
-      g->max_slots = std::max<int>(g->max_slots, B.nloc + B.nvirt);
-      g->max_virt = std::max<int>(g->max_virt, B.nvirt);
-      g->max_cout = std::max<int>(g->max_cout, B.ncout);
-      g->max_block_depth = std::max<int64_t>(g->max_block_depth, B.dmax + 1);
-      pre_dn += bdmax[b] * (int64_t)m.size();
-      p0 += (int64_t)m.size();
-    }
-    phase("emit");
-    for (int64_t i = 0; i < n; ++i) {
-      int64_t P = pos[i];
-      if (dl[P] == -2) dl[P] = (int32_t)local[g->down[i]];
-    }
-    g->sum_dn = pre_dn;
-    g->max_nloc = (int)max_load;
-    int kr = 1;
-    while (int64_t(kr) * bs < max_load) kr *= 2;
-    g->kr = kr;
-    if (g->max_virt > bs || g->max_cout > bs)
-      return fail(DDR_ERR_CAPACITY, "too many inter-workgroup edges in one workgroup");
-    phase("schedule");
-    if (dbg) {  // schedule fingerprint (FNV-1a over the emitted arrays)
-      unsigned long long h = 1469598103934665603ull;
-      auto mix = [&](const std::vector<int32_t>& v) {
-        for (int32_t x : v) h = (h ^ (unsigned)x) * 1099511628211ull;
-      };
-      mix(ref); mix(offs); mix(upb); mix(upc); mix(dl); mix(cut); mix(xoff); mix(uplist); mix(xlist);
-      mix(v_edge); mix(v_off); mix(v_dloc); mix(cout_loc);
-      fprintf(stderr, "[part] schedule fingerprint %016llx\n", h);
-    }
-    // reference-order views for the q' gather: pos_of_ref, block_of_pos, and per block its local
-    // indices in ascending reference order (a stable counting sort of the reach ids by block)
-    H.pos_of_ref.resize(n);
-    H.block_of_pos.resize(n);
-    H.rs_loc.resize(n);
-    H.rs_ref.resize(n);
-    {
-      std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
-      for (int64_t i = 0; i < n; ++i) {
-        H.pos_of_ref[i] = pos[i];
-        H.block_of_pos[pos[i]] = (int32_t)g->block_of[i];
-        const int64_t k = fillb[g->block_of[i]]++;
-        H.rs_ref[k] = (int32_t)i;
-        H.rs_loc[k] = local[i];
-      }
-    }
-    phase("views");
-    if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) break;
-    ddr_status st = upload_schedule(g.get());
-    if (st) return st;
-    phase("upload");
+    if (outcome == kPackResplit) continue;
     break;
   }
+  g->n_pieces = (int64_t)pt.count();
+  if ((st = finalize_blocks(g.get(), plan, pr))) return st;
+  const int64_t nblocks = pr.nblocks;
+  // ---- emit the schedule -----------------------------------------------------------------
+  g->block_of.assign(n, 0);
+  for (int64_t i = 0; i < n; ++i) g->block_of[i] = pr.block_of_piece[piece[i]];
+  const std::vector<int64_t>& bdmax = pr.bdmax;
+  std::vector<int32_t> offv(n);
+  for (int64_t i = 0; i < n; ++i) offv[i] = bdmax[g->block_of[i]] - dloc_piece[i];
+  // internal order (block, tick offset, reference index): two stable counting sorts over the
+  // ascending reach ids, by offset and then by block (O(n), no comparison sort)
+  std::vector<int64_t> bstart(nblocks + 1, 0);
+  std::vector<int32_t> order_all(n);
+  {
+    int64_t omax = 0;
+    for (int64_t b = 0; b < nblocks; ++b) omax = std::max(omax, bdmax[b]);
+    std::vector<int64_t> oc(omax + 2, 0);
+    for (int64_t i = 0; i < n; ++i) oc[offv[i] + 1]++;
+    for (int64_t o = 0; o <= omax; ++o) oc[o + 1] += oc[o];
+    std::vector<int32_t> by_off(n);
+    for (int64_t i = 0; i < n; ++i) by_off[oc[offv[i]]++] = (int32_t)i;
+    for (int64_t i = 0; i < n; ++i) bstart[g->block_of[i] + 1]++;
+    for (int64_t b = 0; b < nblocks; ++b) bstart[b + 1] += bstart[b];
+    std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
+    for (int64_t j = 0; j < n; ++j) {
+      const int32_t i = by_off[j];
+      order_all[fillb[g->block_of[i]]++] = i;
+    }
+  }
+  phase("members");
+  std::vector<int32_t> pos(n), local(n);
+  HostSchedule& H = g->hs;
+  H = HostSchedule{};
+  std::vector<int32_t>&ref = H.ref, &offs = H.off, &upb = H.upb, &upc = H.upc, &dl = H.dloc, &cut = H.cut,
+                      &xoff = H.xoff, &uplist = H.uplist, &xlist = H.xlist, &v_edge = H.v_edge, &v_off = H.v_off,
+                      &v_dloc = H.v_dloc, &cout_loc = H.cout_loc;
+  ref.resize(n);
+  offs.resize(n);
+  upb.resize(n);
+  upc.resize(n);
+  dl.resize(n);
+  cut.assign(n, -1);
+  xoff.assign(n, -1);
+  std::vector<int32_t> edge_id(n, -1);
+  for (int64_t P = 0; P < n; ++P) {
+    pos[order_all[P]] = (int32_t)P;
+    local[order_all[P]] = (int32_t)(P - bstart[g->block_of[order_all[P]]]);
+  }
+  // Cut edges are numbered in (block, local position) order, i.e. by their index in cout_loc: the
+  // forward kernel derives a cut reach's granule row from B.cout0 + its rank among the block's
+  // cut reaches (route.hip), with no table load in the tick.
+  int64_t eid = 0;
+  for (int64_t P = 0; P < n; ++P) {
+    const int32_t i = order_all[P];
+    if (g->down[i] >= 0 && g->block_of[g->down[i]] != g->block_of[i]) edge_id[i] = (int32_t)eid++;
+  }
+  for (int64_t b = 0; b < nblocks; ++b) {
+    const BlockDesc& B = g->blocks[b];
+    for (int64_t r = 0; r < B.nloc; ++r) {
+      const int64_t P = B.pos0 + r;
+      const int64_t i = order_all[P];
+      ref[P] = (int32_t)i;
+      offs[P] = offv[i];
+      upb[P] = (int32_t)uplist.size();
+      upc[P] = (int32_t)(cnt[i + 1] - cnt[i]);
+      for (int64_t k = cnt[i]; k < cnt[i + 1]; ++k) {
+        int64_t j = col[k];
+        if (g->block_of[j] == b) {
+          uplist.push_back(local[j]);
+        } else {
+          // virtual inflow of cut edge j -> i
+          uplist.push_back((int32_t)(B.nloc + (v_edge.size() - B.virt0)));
+          v_edge.push_back(edge_id[j]);
+          v_off.push_back(offv[i] - 1);
+          v_dloc.push_back((int32_t)r);
+        }
+      }
+      if (upc[P] > 2) {
+        // confluence list: [c, u1, ..., u_{c-1}] at xoff (block-local), see route.hip pack_up
+        xoff[P] = (int32_t)(xlist.size() - B.xl0);
+        xlist.push_back(upc[P]);
+        for (int32_t k = 1; k < upc[P]; ++k) xlist.push_back(uplist[upb[P] + k]);
+      }
+      const int64_t d = g->down[i];
+      dl[P] = (d >= 0 && g->block_of[d] == b) ? local[d] : -1;
+      if (d >= 0 && g->block_of[d] != b) {
+        cut[P] = edge_id[i];
+        cout_loc.push_back((int32_t)r);
+      }
+    }
+  }
+  phase("emit");
+  if (dbg) fprintf(stderr, "[part] schedule fingerprint %016llx\n", schedule_fingerprint(H));
+  // reference-order views for the q' gather: pos_of_ref, block_of_pos, and per block its local
+  // indices in ascending reference order (a stable counting sort of the reach ids by block)
+  H.pos_of_ref.resize(n);
+  H.block_of_pos.resize(n);
+  H.rs_loc.resize(n);
+  H.rs_ref.resize(n);
+  {
+    std::vector<int64_t> fillb(bstart.begin(), bstart.end() - 1);
+    for (int64_t i = 0; i < n; ++i) {
+      H.pos_of_ref[i] = pos[i];
+      H.block_of_pos[pos[i]] = (int32_t)g->block_of[i];
+      const int64_t k = fillb[g->block_of[i]]++;
+      H.rs_ref[k] = (int32_t)i;
+      H.rs_loc[k] = local[i];
+    }
+  }
+  phase("views");
   g->crow = std::move(cnt);
   g->col = std::move(col);
+  if (!(opts && (opts->flags & DDR_BUILD_HOST_ONLY))) {
+    if ((st = upload_schedule(g.get()))) return st;
+    phase("upload");
+  }
   *out = g.release();
   return DDR_OK;
 }

@@ -132,6 +132,7 @@ struct Graph {
   int device = 0;
   std::vector<BlockDesc> blocks;
   int64_t sum_dn = 0;    // sum over blocks of dmax * nloc
+  int64_t n_xlist = 0;   // confluence-list entries over all blocks
   int max_nloc = 0;      // largest block
   int64_t generations = 1;  // ceil(blocks / resident) the packer aimed for (1: all blocks co-resident)
   int64_t resident = 0;     // co-resident workgroups assumed by the packer
@@ -140,6 +141,43 @@ struct Graph {
   bool uploaded = false;
   std::vector<void*> allocations;
 };
+
+// ---- piece-level packing, shared by the host builder (graph.cpp) and the device builder ---------
+// (devgraph.hip).  Pieces are numbered by descending root index, so a child piece (upstream) comes
+// after its parent.
+struct PieceTable {
+  std::vector<int64_t> root;       // root reach (the piece's most downstream reach)
+  std::vector<int64_t> size;       // reaches
+  std::vector<int64_t> dmax;       // max in-piece distance of a member to the root
+  std::vector<int64_t> xl;         // confluence-list entries (members with more than two inflows)
+  std::vector<int64_t> parent;     // piece of down[root], -1 for an outlet piece
+  std::vector<int64_t> dloc_down;  // in-piece distance of down[root] (0 for an outlet piece)
+  std::vector<int64_t> ht_root;    // longest path from the root up to a source
+  std::vector<int64_t> dist_root;  // hops from the root to its outlet
+  size_t count() const { return root.size(); }
+};
+// The packer's state across re-splits (capacity, weighting, generations).
+struct PackPlan {
+  int64_t n = 0, cap = 0, hard_cap = 0, cap_start = 0, min_cap = 0, target = 0, resident = 0, gen = 1;
+  int64_t scap_pct = 80, pack_quant = 1;
+  bool weighted = true, dbg = false;
+  double steps = 8760.0, fac_pow = 1.0;
+  int device = 0;
+  int64_t scap() const { return cap * scap_pct / 100; }  // split threshold of this pass
+};
+struct PackResult {
+  int64_t nblocks = 0, ncut = 0;
+  std::vector<int64_t> block_of_piece, load, bdmax, bv, bc, bx;  // per block: reaches, dmax, virt, cut-outs, xl
+};
+enum { kPackDone = 0, kPackResplit = 1 };
+// bmax: the largest basin (selects the split threshold)
+ddr_status plan_init(int64_t n, int64_t bmax, const ddr_build_opts* opts, PackPlan& plan);
+// Pack the pieces of one split; *outcome = kPackResplit when the plan changed (split again).
+ddr_status pack_pieces(PackPlan& plan, const PieceTable& pt, PackResult& res, int* outcome);
+// Block descriptors and the graph-wide sizes (max slots, KR, ...) of a finished packing.
+ddr_status finalize_blocks(Graph* g, const PackPlan& plan, const PackResult& res);
+unsigned long long schedule_fingerprint(const HostSchedule& H);
+double now_ms();
 
 // error plumbing (capi.cpp)
 void set_error(const std::string& msg);
@@ -161,7 +199,7 @@ void destroy_graph(Graph* g);
 ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                           const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                           int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
-                          int32_t* gage_c);
+                          int64_t out_idx_cap, int32_t* gage_c);
 // Upload a host-built schedule (DDR_BUILD_HOST_ONLY) to the current device; no-op once uploaded.
 ddr_status upload_schedule(Graph* g);
 

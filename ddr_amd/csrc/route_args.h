@@ -110,7 +110,9 @@ hipError_t launch_gauge_daily(const GaugeArgs& a, const R* xsave, int64_t t0, in
 template <typename R>
 hipError_t launch_gauge_daily_seed(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh,
                                    hipStream_t stream);
-// geometry.hip
+// geometry.hip: windows of up to kGeoLongMaxDays days (~89 years; beyond 512 days one workgroup per
+// reach sorts each variable in LDS)
+constexpr int64_t kGeoLongMaxDays = 32768;
 hipError_t launch_geometry_stats(const float* qd, int64_t rs, int64_t ds, int64_t N, int64_t D, const float* n,
                                  const float* p, int64_t p_stride, const float* q, const float* S, float depth_lb,
                                  float bw_lb, float* out, hipStream_t stream);

@@ -87,5 +87,7 @@ def gather_rows(local: torch.Tensor, global_index: torch.Tensor, n_global: int) 
     dist.all_gather(all_rows, pad_rows)
     for i_, r_ in zip(all_idx, all_rows):
         keep = i_ >= 0
-        out[i_[keep]] = r_[keep]
-    return out
+        out[i_[keep]] = r_[keep].detach()
+    # this rank's rows once more from `local` itself: the all-gathered copies carry no gradient, so a
+    # loss over the gathered series back-propagates into this rank's shard as it does with one process
+    return out.index_put((idx,), local)

@@ -48,7 +48,8 @@ def compute_geometry_statistics(n: torch.Tensor, p_spatial: torch.Tensor, q_spat
     """Per-reach temporal statistics (``statistics.py:20-83``): keys ``{var}_{min,max,median,mean}`` for
     depth, top_width, bottom_width, side_slope, hydraulic_radius and discharge, each (N,) float32.
 
-    ``daily_accumulated_discharge`` is (n_days, N) (numpy or tensor), at most 512 days per call.
+    ``daily_accumulated_discharge`` is (n_days, N) (numpy or tensor), up to 32768 days (~89 years) per
+    call: windows beyond 512 days sort each reach's values in LDS (one workgroup per reach).
     Runs on the HIP device (``device``, default the current one); no CPU fallback."""
     if not torch.cuda.is_available():
         raise RuntimeError("compute_geometry_statistics runs on the HIP device only (no CPU fallback)")

@@ -95,11 +95,14 @@ class MuskingumCunge:
     def __init__(self, cfg: Any, device: str | torch.device = "cpu") -> None:
         self.cfg = cfg
         self.device = device
-        # forward coefficient arithmetic of the fused kernel (ops.route ``math``): "faithful" (default:
-        # the reference's operation order and IEEE divisions, pows in fp32 faithful-class arithmetic --
-        # the accuracy class of the reference's own Sleef powf), "exact" (correctly rounded pow:
-        # bit-identical to the oracle) or "fast"; cfg.params.routing_math or DDR_ROUTING_MATH override
-        self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "faithful")
+        # forward coefficient arithmetic of the fused kernel, the same default as ops.route ``math``:
+        # "exact" (default: the reference's operation order, IEEE division, correctly rounded pow --
+        # bit-identical to the oracle), "faithful" (the same order and divisions, pows in fp32
+        # faithful-class arithmetic, the accuracy class of the reference's own Sleef powf; what
+        # bench.py times) or "fast"; cfg.params.routing_math or DDR_ROUTING_MATH select another
+        self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "exact")
+        if self.math not in ("exact", "faithful", "fast"):
+            raise ValueError(f"routing_math must be 'exact', 'faithful' or 'fast', not {self.math!r}")
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None

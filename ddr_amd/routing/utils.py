@@ -11,7 +11,6 @@ network, so callers that pass a mapper (``compute_hotstart_discharge``) reach th
 
 from __future__ import annotations
 
-import ctypes as C
 import logging
 from collections.abc import Callable
 from typing import Any
@@ -81,25 +80,6 @@ class PatternMapper:
 
     def getSparseIndices(self) -> tuple[torch.Tensor, torch.Tensor]:
         return self.crow_indices, self.col_indices
-
-    @staticmethod
-    def inverse_diag_fill(data_vector: torch.Tensor) -> torch.Tensor:
-        n = data_vector.shape[0]
-        return torch.diag(data_vector.flip(0))
-
-    @staticmethod
-    def diag_aug(datvec: torch.Tensor, n: int, constant_diags: list[float], constant_offsets: list[int]) -> torch.Tensor:
-        out = datvec.clone()
-        for c in constant_diags:
-            out = torch.cat((out, torch.zeros(n, dtype=datvec.dtype) + c), nsdim(datvec) or 0)
-        return out
-
-
-def nsdim(datvec: torch.Tensor) -> int | None:
-    for i in range(datvec.ndim):
-        if datvec.shape[i] > 1:
-            return i
-    return None
 
 
 def get_network_idx(mapper: PatternMapper) -> tuple[torch.Tensor, torch.Tensor]:
@@ -194,4 +174,3 @@ __all__ = [
     "_fill_row_indices_vectorized", "_compute_row_indices_gpu",
 ]
 
-_ = C  # ctypes kept for symmetry with ops.py

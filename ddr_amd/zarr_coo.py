@@ -54,6 +54,11 @@ def _zstd():
 def zstd_decompress(buf: bytes, size_hint: int) -> bytes:
     lib = _zstd()
     n = lib.ZSTD_getFrameContentSize(buf, len(buf))
+    # the chunk's size is known from the array metadata: a frame declaring more is corrupt (or hostile)
+    # and is refused before anything is allocated for it; an undeclared size decompresses into
+    # size_hint bytes at most (ZSTD_decompress fails if the content does not fit)
+    if n < (1 << 62) and int(n) > int(size_hint):
+        raise ValueError(f"corrupt zstd chunk: declares {int(n)} bytes, the chunk holds at most {int(size_hint)}")
     cap = int(n) if n < (1 << 62) else int(size_hint)
     out = C.create_string_buffer(max(cap, 1))
     r = lib.ZSTD_decompress(out, cap, buf, len(buf))

@@ -97,7 +97,8 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
  *        [sub_off[g], sub_off[g+1]) of rows (downstream) / cols (upstream); gage_idx[g] (CONUS).
  *   out: active[n_active] CONUS ids of the union's reaches, ascending (capacity: min(n_conus,
  *        2 E + n_gauges)); crow[n_active + 1], col[nnz] canonical CSR of the compressed union
- *        (capacity of col: E); out_off[n_gauges + 1], out_idx (capacity E + n_gauges): outflow_idx
+ *        (capacity of col: E); out_off[n_gauges + 1], out_idx (out_idx_cap entries; E + n_gauges
+ *        suffices for consistent subsets, DDR_ERR_ARG when the lists would exceed it): outflow_idx
  *        of each gauge, the compressed upstream reaches of its reach ascending (itself when it has
  *        none); gage_c[n_gauges] each gauge's compressed index.
  * Rejects non-lower-triangular entries (DDR_ERR_NOT_LOWER) and a union in which a reach drains into
@@ -105,7 +106,7 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
 ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                               const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                               int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
-                              int32_t* gage_c);
+                              int64_t out_idx_cap, int32_t* gage_c);
 /* Upload the schedule of a graph built with DDR_BUILD_HOST_ONLY to the current HIP device (no-op
  * if already uploaded).  The host build needs no device: it can run on any host thread (e.g. a
  * data-loader worker preparing the next training batch, merit.py:197-223) while the device routes
@@ -264,7 +265,7 @@ ddr_status ddr_gauge_daily_seed_f64(int64_t G, int64_t T, int64_t t0, int64_t L,
 
 /* Per-reach temporal statistics of the trapezoid geometry (src/ddr/geometry/statistics.py:20-83):
  * q_daily holds the daily accumulated discharge, element (reach, day) at
- * reach * reach_stride + day * day_stride (1 <= days <= 512); out is (24, n): for the variables
+ * reach * reach_stride + day * day_stride (1 <= days <= 32768); out is (24, n): for the variables
  * depth, top_width, bottom_width, side_slope, hydraulic_radius, discharge (in this order) the rows
  * min, max, median, mean (NaN skipped as numpy's nan* reductions).  Device pointers, float32. */
 ddr_status ddr_geometry_stats_f32(const float* q_daily, int64_t reach_stride, int64_t day_stride, int64_t n,

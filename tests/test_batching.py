@@ -108,6 +108,12 @@ def test_collate_rejects_bad_unions():
     # a lone headwater gauge: one reach, outflow_idx = itself
     cb = collate_gauges(5, [(np.zeros(0, np.int32), np.zeros(0, np.int32), 3)])
     assert cb.active.tolist() == [3] and cb.outflow_idx[0].tolist() == [0] and cb.col.size == 0
+    # inconsistent subsets: three gauges on reach 3, whose three inflow edges only the
+    # first subset holds, need 9 outflow entries against E + G = 6: refused, not written past the end
+    empty = (np.zeros(0, np.int32), np.zeros(0, np.int32), 3)
+    with pytest.raises(_lib.DDRError) as e:
+        collate_gauges(5, [(np.array([3, 3, 3]), np.array([0, 1, 2]), 3), empty, empty])
+    assert e.value.code == _lib.DDR_ERR_ARG and "out_idx_cap" in str(e.value)
 
 
 def test_collate_conus_scale_union_matches_numpy():
@@ -141,3 +147,14 @@ def test_collate_conus_scale_union_matches_numpy():
                       shape=(len(active), len(active))).tocsr()
     np.testing.assert_array_equal(cb.crow, a.indptr)
     np.testing.assert_array_equal(cb.col, a.indices)
+
+
+def test_zstd_frame_larger_than_chunk_is_refused():
+    """A frame whose header declares more bytes than the chunk can hold raises before any
+    allocation of that size; a well-formed frame decodes."""
+    from ddr_amd.zarr_coo import zstd_compress, zstd_decompress
+
+    frame = zstd_compress(np.arange(64, dtype=np.int32).tobytes())
+    assert np.array_equal(np.frombuffer(zstd_decompress(frame, 256), np.int32), np.arange(64))
+    with pytest.raises(ValueError, match="declares 256 bytes"):
+        zstd_decompress(frame, 16)

@@ -185,6 +185,46 @@ def _objective_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
+def _gather_grad_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from ddr_amd.distributed import gather_rows
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows_of = [np.array([4, 0, 2]), np.array([1, 3])]  # global row index of each rank's local rows
+    base = torch.arange(15, dtype=torch.float64).reshape(5, 3)
+    local = (base[torch.from_numpy(rows_of[rank])] + 1.0).requires_grad_(True)
+    full = gather_rows(local, torch.from_numpy(rows_of[rank]), 5)
+    W = torch.arange(15, dtype=torch.float64).reshape(5, 3) * 0.5 - 2.0
+    (full * W).sum().backward()
+    out[rank] = (full.detach().numpy(), local.grad.numpy().copy(), rows_of[rank])
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_rows_backpropagates():
+    """A loss over the gathered rows gives every rank the gradient of its own rows: the same
+    gradient a single process gets from ``loss(full).backward()``."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    world = 2
+    ctx = mp.get_context("spawn")
+    out = ctx.Manager().dict()
+    procs = [ctx.Process(target=_gather_grad_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    W = np.arange(15, dtype=np.float64).reshape(5, 3) * 0.5 - 2.0
+    full_ref = np.arange(15, dtype=np.float64).reshape(5, 3) + 1.0
+    for r in range(world):
+        full, g, rows = out[r]
+        np.testing.assert_array_equal(full, full_ref)
+        np.testing.assert_array_equal(g, W[rows])  # single-process gradient of these rows
+
+
 def test_two_rank_c3_objective_allreduce_and_gather():
     """The multi-GPU C3 step at world size 2 (gloo): gauges follow their basins, each rank's L1 is its
     share of the global mean, the all-reduced gradient equals the single-process one and gather_rows

@@ -173,3 +173,26 @@ def test_c4_pipeline_matches_oracle(cuda):
     for k, v in got.items():
         tol = 1e-6 if k.endswith("_mean") else 0.0
         assert maxrel(v, orc[k]) <= tol, k
+
+
+@pytest.mark.parametrize("D", [513, 1100])
+def test_geometry_statistics_long_window(cuda, D):
+    """Windows beyond 512 days (multi-year predictor runs; the reference has no cap,
+    statistics.py:20-83) take the workgroup-per-reach LDS sort: equal to the oracle, NaN days skipped."""
+    rng = np.random.default_rng(D)
+    N = 300
+    n = rng.uniform(0.015, 0.25, N).astype(np.float32)
+    p = rng.uniform(1.0, 200.0, N).astype(np.float32)
+    q = rng.uniform(0.0, 1.0, N).astype(np.float32)
+    slope = rng.uniform(1e-3, 0.05, N).astype(np.float32)
+    qd = rng.lognormal(0.0, 2.0, (D, N)).astype(np.float32)
+    qd[rng.random((D, N)) < 0.01] = np.nan
+    qd[:, 7] = np.nan  # a reach without a valid day
+    got = compute_geometry_statistics(torch.from_numpy(n), torch.from_numpy(p), torch.from_numpy(q),
+                                      torch.from_numpy(slope), qd)
+    orc = O.geometry_statistics(n, p, q, slope, qd)
+    for k, v in got.items():
+        assert np.array_equal(np.isnan(v), np.isnan(orc[k])), k
+        ok = ~np.isnan(orc[k])
+        tol = 1e-6 if k.endswith("_mean") else 0.0
+        assert maxrel(v[ok], orc[k][ok]) <= tol, (D, k)

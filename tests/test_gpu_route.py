@@ -280,6 +280,9 @@ def test_forced_timeout_raises_on_next_call(cuda):
     with pytest.raises(_lib.DDRError) as e:
         run_hip(case, cuda, gkw=gkw, grads=False)
     assert e.value.code == _lib.DDR_ERR_TIMEOUT
+    # the message names the launch that timed out (its graph handle), not the call that reported it
+    assert f"graph {hex(bad['graph'].handle.value)}" in str(e.value), str(e.value)
+    assert "forward launch" in str(e.value)
     check_status()  # reported once
     ok = run_hip(case, cuda, gkw=gkw)
     assert np.isfinite(ok["runoff"]).all()
