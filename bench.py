@@ -212,7 +212,10 @@ def main():
     ap.add_argument("--stream", type=int, default=0,
                     help="C3, 1 GPU: also time K training steps over K different batches (a new gauge-union "
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
-    ap.add_argument("--stream-workers", type=int, default=4)
+    ap.add_argument("--stream-workers", type=int, default=4, help="host builder threads (--stream-builder host)")
+    ap.add_argument("--stream-builder", default="device", choices=["device", "host"],
+                    help="where the per-batch graph is built: on the device (ddr_graph_build_device, one builder "
+                         "thread on its own stream) or on host threads (ddr_graph_build + upload)")
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
     ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
@@ -473,8 +476,9 @@ def time_training_stream(args, dev):
     consts = RouteConsts()
     torch.cuda.synchronize()
     warm = 2
+    on_dev = args.stream_builder == "device"
     pf = GraphPrefetcher(((data[k % M]["net"].n, data[k % M]["net"].rows, data[k % M]["net"].cols, k % M)
-                          for k in range(K + warm)), workers=args.stream_workers, steps_hint=T)
+                          for k in range(K + warm)), workers=args.stream_workers, steps_hint=T, on_device=on_dev)
     per = []
     t_start = None
     for k in range(K + warm):
@@ -502,9 +506,12 @@ def time_training_stream(args, dev):
     timed = time.perf_counter() - t_start
     pf.close()
     rs = sum(b["reaches"] for b in per) * (T - 1)
+    waits = [b["graph_wait_ms"] for b in per]
     return {"steps": K, "ms_per_step": timed / K * 1e3, "value": rs / timed, "unit": "reach-timesteps/s",
-            "graph_workers": args.stream_workers, "batches": per,
-            "note": f"new adjacency + graph build per step (overlapped on host threads), {M} distinct batches cycled"}
+            "graph_builder": args.stream_builder, "graph_workers": 1 if on_dev else args.stream_workers,
+            "graph_wait_ms_mean": float(np.mean(waits)) if waits else None, "batches": per,
+            "note": (f"new adjacency + graph build per step ({'on the device, builder thread + stream' if on_dev else 'on host threads'}"
+                     f", overlapped with training), {M} distinct batches cycled")}
 
 
 def time_dropin(args, net, at, u, qprime, W, dev):

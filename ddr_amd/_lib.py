@@ -76,9 +76,13 @@ _I64 = C.c_int64
 _I32 = C.c_int32
 _SIGS = {
     "ddr_graph_build": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), C.POINTER(C.c_void_p)]),
+    "ddr_graph_build_device": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P, C.POINTER(C.c_void_p)]),
+    "ddr_graph_fingerprint": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "ddr_graph_destroy": (C.c_int, [_P]),
     "ddr_graph_upload": (C.c_int, [_P]),
     "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "ddr_collate_gauges_device": (C.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _I64, C.POINTER(C.c_int64), _P, _P,
+                                            C.POINTER(C.c_int64), _P, _P, _P, _P, _I64, _P, _P]),
     "ddr_graph_get_info": (C.c_int, [_P, C.POINTER(GraphInfo)]),
     "ddr_graph_csr": (C.c_int, [_P, _P, _P]),
     "ddr_graph_structure": (C.c_int, [_P, _P, _P, _P, _P]),

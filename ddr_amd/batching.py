@@ -122,3 +122,76 @@ def construct_network_matrix(batch, subsets):
     c = cb.active[cols]
     coo = sp.coo_matrix((np.ones(len(r)), (r, c)), shape=(cb.n_conus, cb.n_conus))
     return coo, cb.gage_idx, cb.gage_catchment
+
+
+@dataclass
+class DeviceBatch:
+    """The gauge union computed on the device (``ddr_collate_gauges_device``): every array a device
+    tensor; ``graph()`` builds the routing schedule on the device from the compressed COO, so nothing
+    per reach leaves the device between the zarr subsets and the routing launch."""
+    n_conus: int
+    active: "torch.Tensor"       # (n,) int32 CONUS ids, ascending
+    rows: "torch.Tensor"         # (nnz,) int32 compressed COO (downstream)
+    cols: "torch.Tensor"         # (nnz,) int32 (upstream, ascending)
+    crow: "torch.Tensor"         # (n + 1,) int64 canonical CSR
+    col: "torch.Tensor"          # (nnz,) int32
+    out_off: "torch.Tensor"      # (G + 1,) int64
+    out_idx: "torch.Tensor"      # int32
+    gage_c: "torch.Tensor"       # (G,) int32
+    gage_idx: list
+
+    @property
+    def n(self) -> int:
+        return int(self.active.numel())
+
+    def graph(self, **kw):
+        from .graph import RiverGraph
+
+        return RiverGraph(self.n, self.rows, self.cols, **kw)
+
+    def outflow_idx(self) -> list:
+        off = self.out_off.cpu().numpy()
+        idx = self.out_idx.cpu().numpy().astype(np.int64)
+        return [idx[off[g]:off[g + 1]] for g in range(len(off) - 1)]
+
+    def to_host(self) -> CollatedBatch:
+        return CollatedBatch(self.n_conus, self.active.cpu().numpy().astype(np.int64), self.crow.cpu().numpy(),
+                             self.col.cpu().numpy().astype(np.int64), self.outflow_idx(),
+                             [int(x) for x in self.gage_c.cpu().numpy()], list(self.gage_idx), [None] * len(self.gage_idx))
+
+
+def collate_gauges_device(n_conus: int, subsets, device=None, stream=None) -> DeviceBatch:
+    """:func:`collate_gauges` on the device.  ``subsets``: ``(rows, cols, gage_idx)`` in CONUS numbering,
+    host arrays or device tensors; they are concatenated on the device."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    subsets = list(subsets)
+    G = len(subsets)
+    with torch.cuda.device(dev):
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        with torch.cuda.stream(st):
+            t = lambda a: torch.as_tensor(a).reshape(-1).to(dev, torch.int32)  # noqa: E731
+            rows = torch.cat([t(r) for r, _, _ in subsets]) if G else torch.zeros(0, dtype=torch.int32, device=dev)
+            cols = torch.cat([t(c) for _, c, _ in subsets]) if G else torch.zeros(0, dtype=torch.int32, device=dev)
+            if rows.shape != cols.shape:
+                raise ValueError("every subset needs as many cols as rows")
+            gidx_list = [int(g) for _, _, g in subsets]
+            gidx = torch.tensor(gidx_list, dtype=torch.int32, device=dev)
+            E = rows.numel()
+            cap = int(min(n_conus, 2 * E + G))
+            i32 = dict(dtype=torch.int32, device=dev)
+            active = torch.empty(max(cap, 1), **i32)
+            rows_c, cols_c, col = (torch.empty(max(E, 1), **i32) for _ in range(3))
+            crow = torch.empty(cap + 1, dtype=torch.int64, device=dev)
+            out_off = torch.empty(G + 1, dtype=torch.int64, device=dev)
+            out_idx = torch.empty(max(E + G, 1), **i32)
+            gage_c = torch.empty(max(G, 1), **i32)
+        na, nnz = C.c_int64(), C.c_int64()
+        _lib.check(_lib.load().ddr_collate_gauges_device(
+            int(n_conus), G, E, rows.data_ptr(), cols.data_ptr(), gidx.data_ptr(), active.data_ptr(), cap, C.byref(na),
+            rows_c.data_ptr(), cols_c.data_ptr(), C.byref(nnz), crow.data_ptr(), col.data_ptr(), out_off.data_ptr(),
+            out_idx.data_ptr(), out_idx.numel(), gage_c.data_ptr(), st.cuda_stream))
+    n, k = na.value, nnz.value
+    return DeviceBatch(int(n_conus), active[:n], rows_c[:k], cols_c[:k], crow[:n + 1], col[:k], out_off,
+                       out_idx[:int(out_off[-1].item()) if G else 0], gage_c[:G], gidx_list)

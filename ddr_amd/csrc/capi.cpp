@@ -382,6 +382,46 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
   })
 }
 
+ddr_status ddr_graph_build_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                  const ddr_build_opts* opts, void* stream, ddr_graph** out) {
+  DDR_GUARD({
+    if (!out) return fail(DDR_ERR_ARG, "null out");
+    Graph* g = nullptr;
+    ddr_status st = build_graph_device(n, e, rows, cols, opts, static_cast<hipStream_t>(stream), &g);
+    if (st) return st;
+    *out = reinterpret_cast<ddr_graph*>(g);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_fingerprint(const ddr_graph* gh, uint64_t* fp) {
+  DDR_GUARD({
+    if (!gh || !fp) return fail(DDR_ERR_ARG, "null argument");
+    const Graph* g = reinterpret_cast<const Graph*>(gh);
+    HostSchedule H;
+    if (g->uploaded) {
+      ddr_status st = device_schedule_to_host(g, H);
+      if (st) return st;
+    } else {
+      H = g->hs;
+    }
+    unsigned long long h = schedule_fingerprint(H);
+    auto mix = [&](const std::vector<int32_t>& v) {
+      for (int32_t x : v) h = (h ^ (unsigned)x) * 1099511628211ull;
+    };
+    mix(H.pos_of_ref);
+    mix(H.block_of_pos);
+    mix(H.rs_loc);
+    mix(H.rs_ref);
+    for (const BlockDesc& B : g->blocks) {
+      mix({B.pos0, B.nloc, B.virt0, B.nvirt, B.cout0, B.ncout, B.dmax, B.nxl, (int32_t)B.pre_dn,
+           (int32_t)(B.pre_dn >> 32), B.xl0});
+    }
+    *fp = h;
+    return DDR_OK;
+  })
+}
+
 ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                               const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                               int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
@@ -389,6 +429,18 @@ ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* 
   DDR_GUARD({
     return collate_gauges(n_conus, n_gauges, sub_off, rows, cols, gage_idx, active, n_active, crow, col, nnz,
                           out_off, out_idx, out_idx_cap, gage_c);
+  })
+}
+
+ddr_status ddr_collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
+                                     const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,
+                                     int64_t* n_active, int32_t* rows_c, int32_t* cols_c, int64_t* nnz, int64_t* crow,
+                                     int32_t* col, int64_t* out_off, int32_t* out_idx, int64_t out_idx_cap,
+                                     int32_t* gage_c, void* stream) {
+  DDR_GUARD({
+    return collate_gauges_device(n_conus, n_gauges, e, rows, cols, gage_idx, active, active_cap, n_active, rows_c,
+                                 cols_c, nnz, crow, col, out_off, out_idx, out_idx_cap, gage_c,
+                                 static_cast<hipStream_t>(stream));
   })
 }
 
@@ -431,6 +483,7 @@ ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
 ddr_status ddr_graph_csr(const ddr_graph* gh, int64_t* crow, int64_t* col) {
   if (!gh || !crow || (!col && reinterpret_cast<const Graph*>(gh)->nnz > 0)) return fail(DDR_ERR_ARG, "null argument");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (g->device_built) DDR_GUARD({ return device_views_to_host(g, crow, col, nullptr, nullptr, nullptr, nullptr); })
   std::memcpy(crow, g->crow.data(), sizeof(int64_t) * (g->n + 1));
   if (g->nnz) std::memcpy(col, g->col.data(), sizeof(int64_t) * g->nnz);
   return DDR_OK;
@@ -439,6 +492,7 @@ ddr_status ddr_graph_csr(const ddr_graph* gh, int64_t* crow, int64_t* col) {
 ddr_status ddr_graph_structure(const ddr_graph* gh, int64_t* down, int64_t* dist, int64_t* basin, int64_t* block) {
   if (!gh) return fail(DDR_ERR_ARG, "null graph");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (g->device_built) DDR_GUARD({ return device_views_to_host(g, nullptr, nullptr, down, dist, basin, block); })
   const size_t b = sizeof(int64_t) * g->n;
   if (down) std::memcpy(down, g->down.data(), b);
   if (dist) std::memcpy(dist, g->dist.data(), b);

@@ -1,0 +1,979 @@
+// On-device river-graph builder (BASELINE north star (1): "a CSR/level-set converter builds on device
+// from the zarr COO").  Input: the COO adjacency in device memory (row = downstream reach, col =
+// upstream reach, the ddr-engine contract, engine/src/ddr_engine/core/zarr_io.py:7-76).  Output: the
+// same Graph as the host builder (graph.cpp) -- validation, canonical CSR (scipy .tocsr(),
+// merit.py:197-223), dendritic structure, stem-preserving basin split, and the per-workgroup tick
+// schedule -- bit for bit, with every O(n) pass on the device:
+//
+//   validate + down[] (atomicCAS: a reach with two downstream reaches, a duplicate edge) -> CSR (one
+//   stable radix sort of the reaches by their downstream reach: the children of each row come out
+//   ascending) -> distance to outlet and basin (pointer jumping, log2(depth) rounds) -> subtree size
+//   and height, then the split (per basin one workgroup walks its reaches level by level, deepest
+//   first: a reach's children are final when its level runs) -> pieces (nearest piece root by
+//   pointer jumping; pieces numbered by descending root index as on the host) -> piece table ->
+//   HOST: pack_pieces (the packer works on the few thousand pieces, graph.cpp) -> schedule emission
+//   (sort by (block, tick offset, reach); prefix sums number the cut edges, virtual inflows,
+//   upstream lists and confluence lists in position order).
+//
+// The host reads the device twice per split pass (a count, then the piece table); everything per
+// reach stays on the device.  Temporaries are stream-ordered (hipMallocAsync) on the build stream.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <memory>
+#include <vector>
+
+#include "internal.h"
+
+namespace ddr {
+
+namespace {
+
+constexpr int kTB = 256;  // threads per workgroup of the flat kernels
+inline unsigned nblk(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + kTB - 1) / kTB); }
+inline int bits_for(uint64_t maxval) {  // radix-sort key bits covering [0, maxval]
+  int b = 1;
+  while (b < 64 && (maxval >> b) != 0) ++b;
+  return b;
+}
+
+// error words (min over offending entries): edge out of range, edge not below the diagonal, duplicate
+// edge, reach with two downstream reaches
+enum { kErrRange = 0, kErrLower = 1, kErrDup = 2, kErrDend = 3, kErrWords = 4 };
+
+__global__ void k_iota(int32_t* v, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] = (int32_t)i;
+}
+
+// down[c] = r for every edge (r, c); deg[r] = number of upstream reaches
+__global__ void k_coo(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols, int32_t* down, int32_t* deg,
+                      unsigned long long* err) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= e) return;
+  const int32_t r = rows[k], c = cols[k];
+  if (r < 0 || r >= n || c < 0 || c >= n) {
+    atomicMin(err + kErrRange, (unsigned long long)k);
+    return;
+  }
+  if (c >= r) {
+    atomicMin(err + kErrLower, (unsigned long long)k);
+    return;
+  }
+  const int32_t old = atomicCAS(down + c, -1, r);
+  if (old == -1) atomicAdd(deg + r, 1);
+  else if (old == r) atomicMin(err + kErrDup, (unsigned long long)k);
+  else atomicMin(err + kErrDend, (unsigned long long)c);
+}
+
+// sort key of reach c for the CSR: its downstream reach (outlets last)
+__global__ void k_down_key(int64_t n, const int32_t* down, uint32_t* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) key[i] = down[i] < 0 ? (uint32_t)n : (uint32_t)down[i];
+}
+
+// pointer jumping: p = parent (a root points to itself), d = hops to p
+__global__ void k_jump_init(int64_t n, const int32_t* down, const uint8_t* stop, int32_t* p, int32_t* d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool r = down[i] < 0 || (stop && stop[i]);
+  p[i] = r ? (int32_t)i : down[i];
+  d[i] = r ? 0 : 1;
+}
+__global__ void k_jump(int64_t n, const int32_t* p, const int32_t* d, int32_t* p2, int32_t* d2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t q = p[i];
+  p2[i] = p[q];
+  d2[i] = d[i] + d[q];
+}
+
+// basin sizes, deepest reach, outlet count
+__global__ void k_stats(int64_t n, const int32_t* down, const int32_t* basin, const int32_t* dist, int32_t* bsize,
+                        int32_t* agg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  atomicAdd(bsize + basin[i], 1);
+  atomicMax(agg + 0, dist[i]);
+  if (down[i] < 0) atomicAdd(agg + 1, 1);
+}
+__global__ void k_bmax(int64_t n, const int32_t* down, const int32_t* bsize, int32_t* agg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && down[i] < 0) atomicMax(agg + 2, bsize[i]);
+}
+
+// level-order key: basin-major, deepest level first
+__global__ void k_level_key(int64_t n, const int32_t* basin, const int32_t* dist, int64_t D, uint64_t* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) key[i] = (uint64_t)basin[i] * (uint64_t)(D + 1) + (uint64_t)(D - dist[i]);
+}
+// level starts (for the max-scan), basin segments
+__global__ void k_level_marks(int64_t n, const uint64_t* key, const int32_t* ord, const int32_t* basin,
+                              int32_t* start_of, int32_t* seg_lo, int32_t* seg_hi) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  start_of[p] = (p == 0 || key[p] != key[p - 1]) ? (int32_t)p : 0;
+  const int32_t b = basin[ord[p]];
+  if (p == 0 || basin[ord[p - 1]] != b) seg_lo[b] = (int32_t)p;
+  if (p == n - 1 || basin[ord[p + 1]] != b) seg_hi[b] = (int32_t)(p + 1);
+}
+// level links: lvl_next[start] = end, lvl_first[end - 1] = start
+__global__ void k_level_links(int64_t n, const uint64_t* key, const int32_t* smax, int32_t* lvl_next) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  if (q == n - 1 || key[q + 1] != key[q]) lvl_next[smax[q]] = (int32_t)(q + 1);
+}
+// outlets in ascending order (one workgroup per basin in the level walks)
+__global__ void k_roots(int64_t n, const int32_t* down, const int32_t* rank, int32_t* roots) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && down[i] < 0) roots[rank[i]] = (int32_t)i;
+}
+__global__ void k_is_outlet(int64_t n, const int32_t* down, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = down[i] < 0 ? 1 : 0;
+}
+
+// Subtree size and height (graph.cpp: sub, ht), one workgroup per basin, deepest level first.
+__global__ void __launch_bounds__(256) k_sub_ht(const int32_t* roots, const int32_t* seg_lo, const int32_t* seg_hi,
+                                                const int32_t* lvl_next, const int32_t* ord, const int32_t* crow,
+                                                const int32_t* col, int32_t* sub, int32_t* ht) {
+  const int32_t root = roots[blockIdx.x];
+  const int32_t lo = seg_lo[root], hi = seg_hi[root];
+  for (int32_t s = lo; s < hi;) {
+    const int32_t e = lvl_next[s];
+    for (int32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
+      const int32_t i = ord[p];
+      int32_t su = 1, h = 0;
+      for (int32_t k = crow[i]; k < crow[i + 1]; ++k) {
+        const int32_t c = col[k];
+        su += sub[c];
+        h = max(h, ht[c] + 1);
+      }
+      sub[i] = su;
+      ht[i] = h;
+    }
+    __threadfence_block();
+    __syncthreads();
+    s = e;
+  }
+}
+
+// Stem-preserving split of the basins larger than scap (graph.cpp build_graph, same rule and the
+// same tie-breaks: the deepest child by (height, size), first in column order; the others by
+// ascending residual size, ties in column order).  Smaller basins stay one piece.
+__global__ void __launch_bounds__(256) k_split(const int32_t* roots, const int32_t* seg_lo, const int32_t* seg_hi,
+                                               const int32_t* lvl_next, const int32_t* ord, const int32_t* crow,
+                                               const int32_t* col, const int32_t* sub, const int32_t* ht,
+                                               int32_t* resid, int32_t* stem, uint8_t* is_root, int64_t scap,
+                                               int64_t lseg) {
+  const int32_t root = roots[blockIdx.x];
+  if (sub[root] <= scap) return;
+  const int32_t lo = seg_lo[root], hi = seg_hi[root];
+  for (int32_t s = lo; s < hi;) {
+    const int32_t e = lvl_next[s];
+    for (int32_t p = s + threadIdx.x; p < e; p += blockDim.x) {
+      const int32_t i = ord[p];
+      const int32_t k0 = crow[i], k1 = crow[i + 1];
+      if (sub[i] <= scap || k0 == k1) {
+        resid[i] = sub[i];
+        stem[i] = ht[i] + 1;
+        continue;
+      }
+      int32_t dc = col[k0];
+      for (int32_t k = k0 + 1; k < k1; ++k) {
+        const int32_t c = col[k];
+        if (ht[c] > ht[dc] || (ht[c] == ht[dc] && sub[c] > sub[dc])) dc = c;
+      }
+      int64_t base = 1 + (int64_t)resid[dc], trib = (int64_t)resid[dc] - stem[dc];
+      const bool keep = base <= scap;
+      if (!keep) {
+        is_root[dc] = 1;
+        base = 1;
+        trib = 0;
+      }
+      int64_t acc = 0;
+      // the other children in (resid, column position) order: a selection per step (few children)
+      int64_t pr = -1, pk = -1;
+      for (int32_t step = 0; step < k1 - k0 - 1; ++step) {
+        int64_t br = 0x7fffffffffffffffll, bk = -1;
+        for (int32_t k = k0; k < k1; ++k) {
+          const int32_t c = col[k];
+          if (c == dc) continue;
+          const int64_t r = resid[c];
+          const bool after = r > pr || (r == pr && k > pk);
+          if (after && (r < br || (r == br && k < bk))) {
+            br = r;
+            bk = k;
+          }
+        }
+        const int32_t c = col[bk];
+        if (trib + acc + br <= scap - lseg && base + acc + br <= scap) acc += br;
+        else is_root[c] = 1;
+        pr = br;
+        pk = bk;
+      }
+      resid[i] = (int32_t)(base + acc);
+      stem[i] = keep ? 1 + stem[dc] : 1;
+    }
+    __threadfence_block();
+    __syncthreads();
+    s = e;
+  }
+}
+
+// piece roots: outlets and the reaches the split cut off
+__global__ void k_piece_flags(int64_t n, const int32_t* down, uint8_t* is_root, int32_t* f) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const bool r = down[i] < 0 || is_root[i];
+  is_root[i] = r ? 1 : 0;
+  f[i] = r ? 1 : 0;
+}
+// piece of every reach (numbered by descending root index: np - 1 - rank of its root) and the piece
+// table (graph.cpp PieceTable); tab is [8][np]
+__global__ void k_pieces(int64_t n, int32_t np, const int32_t* down, const int32_t* prank, const int32_t* q,
+                         int32_t* piece) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) piece[i] = np - 1 - prank[q[i]];
+}
+__global__ void k_piece_table(int64_t n, int32_t np, const int32_t* down, const uint8_t* is_root,
+                              const int32_t* piece, const int32_t* dloc, const int32_t* crow, const int32_t* ht,
+                              const int32_t* dist, int32_t* tab) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = piece[i];
+  atomicAdd(tab + 1 * np + p, 1);
+  atomicMax(tab + 2 * np + p, dloc[i]);
+  const int32_t deg = crow[i + 1] - crow[i];
+  if (deg > 2) atomicAdd(tab + 3 * np + p, deg);
+  if (is_root[i]) {
+    const int32_t d = down[i];
+    tab[0 * np + p] = (int32_t)i;
+    tab[4 * np + p] = d < 0 ? -1 : piece[d];
+    tab[5 * np + p] = d < 0 ? 0 : dloc[d];
+    tab[6 * np + p] = ht[i];
+    tab[7 * np + p] = dist[i];
+  }
+}
+
+// ---- schedule emission --------------------------------------------------------------------------
+__global__ void k_emit_key(int64_t n, const int32_t* piece, const int32_t* dloc, const int32_t* bop,
+                           const int32_t* bdmax, int64_t omax1, int32_t* blk, int32_t* offv, uint64_t* key) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t b = bop[piece[i]];
+  const int32_t o = bdmax[b] - dloc[i];
+  blk[i] = b;
+  offv[i] = o;
+  key[i] = (uint64_t)b * (uint64_t)omax1 + (uint64_t)o;
+}
+// per internal position: reach, counts for the prefix sums
+__global__ void k_emit_counts(int64_t n, const int32_t* order, const int32_t* blk, const int32_t* down,
+                              const int32_t* crow, const int32_t* col, const BlockDesc* blocks, int32_t* pos,
+                              int32_t* local, int32_t* upc, int32_t* cutf, int32_t* nv, int32_t* nx,
+                              int32_t* pos_of_ref, int32_t* block_of_pos) {
+  const int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= n) return;
+  const int32_t i = order[P];
+  const int32_t b = blk[i];
+  pos[i] = (int32_t)P;
+  local[i] = (int32_t)(P - blocks[b].pos0);
+  pos_of_ref[i] = (int32_t)P;
+  block_of_pos[P] = b;
+  const int32_t k0 = crow[i], k1 = crow[i + 1];
+  upc[P] = k1 - k0;
+  const int32_t d = down[i];
+  cutf[P] = (d >= 0 && blk[d] != b) ? 1 : 0;
+  int32_t v = 0;
+  for (int32_t k = k0; k < k1; ++k) v += (blk[col[k]] != b);
+  nv[P] = v;
+  nx[P] = (k1 - k0) > 2 ? (k1 - k0) : 0;
+}
+__global__ void k_emit_cut(int64_t n, const int32_t* order, const int32_t* blk, const int32_t* down,
+                           const int32_t* local, const BlockDesc* blocks, const int32_t* cutf, const int32_t* eid,
+                           const int32_t* nx, const int32_t* xbase, int32_t* ref, int32_t* offs, const int32_t* offv,
+                           int32_t* cut, int32_t* cout_loc, int32_t* edge_of, int32_t* xoff, int32_t* dl) {
+  const int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= n) return;
+  const int32_t i = order[P];
+  const int32_t b = blk[i];
+  const BlockDesc& B = blocks[b];
+  ref[P] = i;
+  offs[P] = offv[i];
+  if (cutf[P]) {
+    cut[P] = eid[P];
+    cout_loc[eid[P]] = (int32_t)(P - B.pos0);
+    edge_of[i] = eid[P];
+  } else {
+    cut[P] = -1;
+    edge_of[i] = -1;
+  }
+  xoff[P] = nx[P] ? xbase[P] - B.xl0 : -1;
+  const int32_t d = down[i];
+  dl[P] = (d >= 0 && blk[d] == b) ? local[d] : -1;
+}
+__global__ void k_emit_up(int64_t n, const int32_t* order, const int32_t* blk, const int32_t* crow,
+                          const int32_t* col, const int32_t* local, const BlockDesc* blocks, const int32_t* upb,
+                          const int32_t* vbase, const int32_t* nx, const int32_t* xbase, const int32_t* offv,
+                          const int32_t* edge_of, int32_t* uplist, int32_t* v_edge, int32_t* v_off,
+                          int32_t* v_dloc, int32_t* xlist) {
+  const int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= n) return;
+  const int32_t i = order[P];
+  const int32_t b = blk[i];
+  const BlockDesc& B = blocks[b];
+  const int32_t k0 = crow[i], k1 = crow[i + 1];
+  const int32_t u0 = upb[P];
+  int32_t v = vbase[P];
+  for (int32_t k = k0; k < k1; ++k) {
+    const int32_t j = col[k];
+    int32_t u;
+    if (blk[j] == b) {
+      u = local[j];
+    } else {
+      // virtual inflow of cut edge j -> i
+      u = B.nloc + (v - B.virt0);
+      v_edge[v] = edge_of[j];
+      v_off[v] = offv[i] - 1;
+      v_dloc[v] = (int32_t)(P - B.pos0);
+      ++v;
+    }
+    uplist[u0 + (k - k0)] = u;
+  }
+  if (nx[P]) {
+    // confluence list: [c, u1, ..., u_{c-1}] (route.hip pack_up)
+    const int32_t x = xbase[P];
+    xlist[x] = k1 - k0;
+    for (int32_t k = 1; k < k1 - k0; ++k) xlist[x + k] = uplist[u0 + k];
+  }
+}
+__global__ void k_rs_loc(int64_t n, const int32_t* rs_ref, const int32_t* local, int32_t* rs_loc) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) rs_loc[k] = local[rs_ref[k]];
+}
+__global__ void k_widen(int64_t n, const int32_t* a, int64_t* b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) b[i] = a[i];
+}
+
+
+// ---- per-batch gauge union on the device (builders.py:55-109, merit.py:197-238) -----------------
+// union of the subsets' (row, col) pairs keyed by the upstream reach (dendritic: one downstream each),
+// active marks of rows, cols and gauges (CONUS numbering)
+__global__ void k_union(int64_t n_conus, int64_t e, const int32_t* rows, const int32_t* cols, int32_t* down,
+                        int32_t* mark, unsigned long long* err) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= e) return;
+  const int32_t r = rows[k], c = cols[k];
+  if (r < 0 || r >= n_conus || c < 0 || c >= n_conus) {
+    atomicMin(err + kErrRange, (unsigned long long)k);
+    return;
+  }
+  if (c >= r) {
+    atomicMin(err + kErrLower, (unsigned long long)k);
+    return;
+  }
+  const int32_t old = atomicCAS(down + c, -1, r);
+  if (old != -1 && old != r) atomicMin(err + kErrDend, (unsigned long long)c);
+  mark[r] = 1;
+  mark[c] = 1;
+}
+__global__ void k_mark_gauges(int64_t n_conus, int64_t G, const int32_t* gidx, int32_t* mark,
+                              unsigned long long* err) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const int32_t x = gidx[g];
+  if (x < 0 || x >= n_conus) atomicMin(err + kErrRange, (unsigned long long)g);
+  else mark[x] = 1;
+}
+// active reaches in CONUS (= topological) order; the compressed downstream of each
+__global__ void k_compress(int64_t n_conus, const int32_t* mark, const int32_t* remap, const int32_t* down,
+                           int32_t* active, int32_t* down_c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_conus || !mark[i]) return;
+  const int32_t a = remap[i];
+  active[a] = (int32_t)i;
+  down_c[a] = down[i] >= 0 ? remap[down[i]] : -1;
+}
+__global__ void k_has_down(int64_t n, const int32_t* down_c, int32_t* f, int32_t* deg) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n) return;
+  f[a] = down_c[a] >= 0 ? 1 : 0;
+  if (down_c[a] >= 0) atomicAdd(deg + down_c[a], 1);
+}
+__global__ void k_union_coo(int64_t n, const int32_t* down_c, const int32_t* kpos, int32_t* rows_c, int32_t* cols_c) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a < n && down_c[a] >= 0) {
+    rows_c[kpos[a]] = down_c[a];
+    cols_c[kpos[a]] = (int32_t)a;
+  }
+}
+// outflow_idx of gauge g: the compressed upstream reaches of its reach (ascending), itself without any
+__global__ void k_outflow_count(int64_t G, const int32_t* gidx, const int32_t* remap, const int32_t* crow,
+                                int32_t* gage_c, int64_t* cnt) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const int32_t x = remap[gidx[g]];
+  gage_c[g] = x;
+  const int32_t d = crow[x + 1] - crow[x];
+  cnt[g] = d > 0 ? d : 1;
+}
+__global__ void k_outflow_fill(int64_t G, const int32_t* gage_c, const int32_t* crow, const int32_t* col,
+                               const int64_t* off, int32_t* out_idx) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const int32_t x = gage_c[g];
+  const int32_t k0 = crow[x], k1 = crow[x + 1];
+  const int64_t o = off[g];
+  if (k1 == k0) out_idx[o] = x;
+  for (int32_t k = k0; k < k1; ++k) out_idx[o + (k - k0)] = col[k];
+}
+
+// Stream-ordered temporaries of one build, released (stream-ordered) when the build returns.
+struct Scratch {
+  hipStream_t s;
+  std::vector<void*> ptrs;
+  hipError_t err = hipSuccess;
+  explicit Scratch(hipStream_t st) : s(st) {}
+  template <typename T>
+  T* get(int64_t n) {
+    void* p = nullptr;
+    const hipError_t e = hipMallocAsync(&p, (size_t)std::max<int64_t>(n, 1) * sizeof(T), s);
+    if (e != hipSuccess) {
+      err = e;
+      return nullptr;
+    }
+    ptrs.push_back(p);
+    return static_cast<T*>(p);
+  }
+  ~Scratch() {
+    for (void* p : ptrs) (void)hipFreeAsync(p, s);
+  }
+};
+
+#define DDR_SCR(ptr)                                                        \
+  do {                                                                      \
+    if (!(ptr)) return ::ddr::hip_fail(scr.err, "device graph: hipMallocAsync"); \
+  } while (0)
+
+template <typename T>
+ddr_status exclusive_sum(Scratch& scr, const T* in, T* out, int64_t n, hipStream_t s) {
+  size_t bytes = 0;
+  DDR_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, s));
+  void* tmp = scr.get<unsigned char>((int64_t)bytes);
+  DDR_SCR(tmp);
+  DDR_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, (int)n, s));
+  return DDR_OK;
+}
+template <typename K>
+ddr_status sort_pairs(Scratch& scr, const K* kin, K* kout, const int32_t* vin, int32_t* vout, int64_t n, int bits,
+                      hipStream_t s) {
+  size_t bytes = 0;
+  DDR_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kin, kout, vin, vout, (int)n, 0, bits, s));
+  void* tmp = scr.get<unsigned char>((int64_t)bytes);
+  DDR_SCR(tmp);
+  DDR_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, bits, s));
+  return DDR_OK;
+}
+
+// Pointer jumping to the nearest ancestor-or-self with down < 0 (or stop[i] != 0): p = that reach,
+// d = hops to it.  `rounds` >= ceil(log2(longest path)) + 1.
+ddr_status jump(Scratch& scr, int64_t n, const int32_t* down, const uint8_t* stop, int rounds, int32_t*& p,
+                int32_t*& d, hipStream_t s) {
+  int32_t* p2 = scr.get<int32_t>(n);
+  int32_t* d2 = scr.get<int32_t>(n);
+  DDR_SCR(p2);
+  DDR_SCR(d2);
+  hipLaunchKernelGGL(k_jump_init, dim3(nblk(n)), dim3(kTB), 0, s, n, down, stop, p, d);
+  for (int r = 0; r < rounds; ++r) {
+    hipLaunchKernelGGL(k_jump, dim3(nblk(n)), dim3(kTB), 0, s, n, p, d, p2, d2);
+    std::swap(p, p2);
+    std::swap(d, d2);
+  }
+  DDR_HIP(hipGetLastError());
+  return DDR_OK;
+}
+
+int log2_rounds(int64_t len) {
+  int r = 1;
+  while ((int64_t(1) << (r - 1)) < len + 1) ++r;
+  return r;
+}
+
+}  // namespace
+
+ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                              const ddr_build_opts* opts, hipStream_t s, Graph** out) {
+  if (n <= 0) return fail(DDR_ERR_ARG, "graph must have at least one reach");
+  if (n >= (int64_t(1) << 31) - 1 || e >= (int64_t(1) << 31) - 1)
+    return fail(DDR_ERR_ARG, "graph too large for int32 reach ids");
+  if (e < 0 || (e > 0 && (!rows || !cols))) return fail(DDR_ERR_ARG, "bad COO arrays");
+  if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) return fail(DDR_ERR_ARG, "a device build cannot be host-only");
+  auto g = std::make_unique<Graph>();
+  g->n = n;
+  g->nnz = e;
+  const bool dbg = getenv("DDR_DEBUG_PART") != nullptr;
+  double tp = now_ms();
+  auto phase = [&](const char* what) {
+    if (!dbg) return;
+    (void)hipStreamSynchronize(s);
+    const double t = now_ms();
+    fprintf(stderr, "[dpart] %-10s %8.2f ms\n", what, t - tp);
+    tp = t;
+  };
+  Scratch scr(s);
+  // persistent device arrays of the graph: CSR + structure views, then the schedule (one allocation)
+  // ---- validation, down[], CSR ----------------------------------------------------------------
+  int32_t* down = scr.get<int32_t>(n);
+  int32_t* deg = scr.get<int32_t>(n + 1);
+  unsigned long long* err = scr.get<unsigned long long>(kErrWords);
+  int32_t* agg = scr.get<int32_t>(4);
+  DDR_SCR(down);
+  DDR_SCR(deg);
+  DDR_SCR(err);
+  DDR_SCR(agg);
+  DDR_HIP(hipMemsetAsync(down, 0xFF, sizeof(int32_t) * n, s));
+  DDR_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (n + 1), s));
+  DDR_HIP(hipMemsetAsync(err, 0xFF, sizeof(unsigned long long) * kErrWords, s));
+  DDR_HIP(hipMemsetAsync(agg, 0, sizeof(int32_t) * 4, s));
+  if (e > 0) hipLaunchKernelGGL(k_coo, dim3(nblk(e)), dim3(kTB), 0, s, n, e, rows, cols, down, deg, err);
+  DDR_HIP(hipGetLastError());
+  // the persistent slab: crow (n+1), col (e), down, dist, basin, block (n each) + the schedule
+  //   ref, off, upb, upc, dloc, cut, xoff, pos_of_ref, block_of_pos, rs_loc, rs_ref (n each),
+  //   uplist (e); v_edge, v_off, v_dloc, cout_loc (<= e each); xlist (<= e + n); blocks (later)
+  int32_t* crow = scr.get<int32_t>(n + 1);
+  DDR_SCR(crow);
+  {
+    ddr_status st = exclusive_sum<int32_t>(scr, deg, crow, n + 1, s);
+    if (st) return st;
+  }
+  uint32_t* dkey = scr.get<uint32_t>(n);
+  uint32_t* dkey2 = scr.get<uint32_t>(n);
+  int32_t* iota = scr.get<int32_t>(n);
+  int32_t* kids = scr.get<int32_t>(n);  // reaches sorted by (downstream, index): the CSR's col
+  DDR_SCR(dkey);
+  DDR_SCR(dkey2);
+  DDR_SCR(iota);
+  DDR_SCR(kids);
+  hipLaunchKernelGGL(k_down_key, dim3(nblk(n)), dim3(kTB), 0, s, n, down, dkey);
+  hipLaunchKernelGGL(k_iota, dim3(nblk(n)), dim3(kTB), 0, s, iota, n);
+  DDR_HIP(hipGetLastError());
+  {
+    ddr_status st = sort_pairs<uint32_t>(scr, dkey, dkey2, iota, kids, n, bits_for((uint64_t)n), s);
+    if (st) return st;
+  }
+  const int32_t* col = kids;  // first e entries
+  // ---- distance to outlet, basin ------------------------------------------------------------
+  int32_t* basin = scr.get<int32_t>(n);
+  int32_t* dist = scr.get<int32_t>(n);
+  DDR_SCR(basin);
+  DDR_SCR(dist);
+  {
+    ddr_status st = jump(scr, n, down, nullptr, log2_rounds(n), basin, dist, s);
+    if (st) return st;
+  }
+  int32_t* bsize = scr.get<int32_t>(n);
+  DDR_SCR(bsize);
+  DDR_HIP(hipMemsetAsync(bsize, 0, sizeof(int32_t) * n, s));
+  hipLaunchKernelGGL(k_stats, dim3(nblk(n)), dim3(kTB), 0, s, n, down, basin, dist, bsize, agg);
+  hipLaunchKernelGGL(k_bmax, dim3(nblk(n)), dim3(kTB), 0, s, n, down, bsize, agg);
+  DDR_HIP(hipGetLastError());
+  unsigned long long herr[kErrWords];
+  int32_t hagg[4];
+  DDR_HIP(hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, s));
+  DDR_HIP(hipMemcpyAsync(hagg, agg, sizeof(hagg), hipMemcpyDeviceToHost, s));
+  DDR_HIP(hipStreamSynchronize(s));
+  phase("csr+tree");
+  // errors in the host builder's order of precedence (graph.cpp): the first bad entry, then
+  // duplicates, then a reach draining into two reaches
+  {
+    const unsigned long long none = ~0ull;
+    auto entry = [&](unsigned long long k, int32_t* rc) -> ddr_status {
+      DDR_HIP(hipMemcpy(rc, rows + k, 4, hipMemcpyDeviceToHost));
+      DDR_HIP(hipMemcpy(rc + 1, cols + k, 4, hipMemcpyDeviceToHost));
+      return DDR_OK;
+    };
+    int32_t rc[2];
+    if (herr[kErrRange] != none || herr[kErrLower] != none) {
+      if (herr[kErrRange] < herr[kErrLower]) return fail(DDR_ERR_ARG, "COO index out of range");
+      ddr_status st = entry(herr[kErrLower], rc);
+      if (st) return st;
+      return fail(DDR_ERR_NOT_LOWER, "adjacency entry (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) +
+                                         ") is not strictly lower triangular (network not topologically sorted)");
+    }
+    if (herr[kErrDup] != none) {
+      ddr_status st = entry(herr[kErrDup], rc);
+      if (st) return st;
+      return fail(DDR_ERR_DUPLICATE, "duplicate edge (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) + ")");
+    }
+    if (herr[kErrDend] != none)
+      return fail(DDR_ERR_NOT_DENDRITIC, "reach " + std::to_string(herr[kErrDend]) + " drains into two reaches");
+  }
+  const int64_t D = hagg[0];          // deepest reach's distance
+  const int64_t n_basins = hagg[1];
+  const int64_t bmax = hagg[2];
+  g->max_depth = D + 1;
+  g->n_basins = n_basins;
+  // ---- level order per basin (deepest level first), subtree size and height --------------------
+  uint64_t* lkey = scr.get<uint64_t>(n);
+  uint64_t* lkey2 = scr.get<uint64_t>(n);
+  int32_t* ord = scr.get<int32_t>(n);
+  int32_t* smark = scr.get<int32_t>(n);
+  int32_t* smax = scr.get<int32_t>(n);
+  int32_t* seg_lo = scr.get<int32_t>(n);
+  int32_t* seg_hi = scr.get<int32_t>(n);
+  int32_t* lvl_next = scr.get<int32_t>(n);
+  int32_t* oflag = scr.get<int32_t>(n + 1);
+  int32_t* orank = scr.get<int32_t>(n + 1);
+  int32_t* roots = scr.get<int32_t>(n_basins);
+  int32_t* sub = scr.get<int32_t>(n);
+  int32_t* ht = scr.get<int32_t>(n);
+  DDR_SCR(lkey); DDR_SCR(lkey2); DDR_SCR(ord); DDR_SCR(smark); DDR_SCR(smax); DDR_SCR(seg_lo); DDR_SCR(seg_hi);
+  DDR_SCR(lvl_next); DDR_SCR(oflag); DDR_SCR(orank); DDR_SCR(roots); DDR_SCR(sub); DDR_SCR(ht);
+  hipLaunchKernelGGL(k_level_key, dim3(nblk(n)), dim3(kTB), 0, s, n, basin, dist, D, lkey);
+  DDR_HIP(hipGetLastError());
+  {
+    ddr_status st = sort_pairs<uint64_t>(scr, lkey, lkey2, iota, ord, n, bits_for((uint64_t)(n - 1) * (uint64_t)(D + 1) + (uint64_t)D), s);
+    if (st) return st;
+  }
+  hipLaunchKernelGGL(k_level_marks, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, ord, basin, smark, seg_lo, seg_hi);
+  DDR_HIP(hipGetLastError());
+  {
+    size_t bytes = 0;
+    DDR_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, bytes, smark, smax, hipcub::Max(), (int)n, s));
+    void* tmp = scr.get<unsigned char>((int64_t)bytes);
+    DDR_SCR(tmp);
+    DDR_HIP(hipcub::DeviceScan::InclusiveScan(tmp, bytes, smark, smax, hipcub::Max(), (int)n, s));
+  }
+  hipLaunchKernelGGL(k_level_links, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, smax, lvl_next);
+  hipLaunchKernelGGL(k_is_outlet, dim3(nblk(n)), dim3(kTB), 0, s, n, down, oflag);
+  DDR_HIP(hipGetLastError());
+  {
+    ddr_status st = exclusive_sum<int32_t>(scr, oflag, orank, n, s);
+    if (st) return st;
+  }
+  hipLaunchKernelGGL(k_roots, dim3(nblk(n)), dim3(kTB), 0, s, n, down, orank, roots);
+  hipLaunchKernelGGL(k_sub_ht, dim3((unsigned)n_basins), dim3(256), 0, s, roots, seg_lo, seg_hi, lvl_next, ord, crow,
+                     col, sub, ht);
+  DDR_HIP(hipGetLastError());
+  phase("sub+ht");
+  // ---- split / piece table / host packing, until the packer accepts --------------------------
+  PackPlan plan;
+  ddr_status st = plan_init(n, bmax, opts, plan);
+  if (st) return st;
+  g->device = plan.device;
+  int32_t* resid = scr.get<int32_t>(n);
+  int32_t* stem = scr.get<int32_t>(n);
+  uint8_t* is_root = scr.get<uint8_t>(n);
+  int32_t* pflag = scr.get<int32_t>(n + 1);
+  int32_t* prank = scr.get<int32_t>(n + 1);
+  int32_t* q = scr.get<int32_t>(n);
+  int32_t* dloc = scr.get<int32_t>(n);
+  int32_t* piece = scr.get<int32_t>(n);
+  int32_t* tab = scr.get<int32_t>(8 * n);
+  DDR_SCR(resid); DDR_SCR(stem); DDR_SCR(is_root); DDR_SCR(pflag); DDR_SCR(prank); DDR_SCR(q); DDR_SCR(dloc);
+  DDR_SCR(piece); DDR_SCR(tab);
+  PieceTable pt;
+  PackResult pr;
+  std::vector<int32_t> htab;
+  for (;;) {
+    const int64_t scap = plan.scap(), lseg = scap / 8;
+    DDR_HIP(hipMemsetAsync(is_root, 0, n, s));
+    hipLaunchKernelGGL(k_split, dim3((unsigned)n_basins), dim3(256), 0, s, roots, seg_lo, seg_hi, lvl_next, ord, crow,
+                       col, sub, ht, resid, stem, is_root, scap, lseg);
+    hipLaunchKernelGGL(k_piece_flags, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, pflag);
+    DDR_HIP(hipGetLastError());
+    DDR_HIP(hipMemsetAsync(pflag + n, 0, 4, s));  // prank[n] = number of pieces
+    if ((st = exclusive_sum<int32_t>(scr, pflag, prank, n + 1, s))) return st;
+    int32_t np = 0;
+    DDR_HIP(hipMemcpyAsync(&np, prank + n, 4, hipMemcpyDeviceToHost, s));
+    if ((st = jump(scr, n, down, is_root, log2_rounds(D + 1), q, dloc, s))) return st;
+    DDR_HIP(hipStreamSynchronize(s));
+    hipLaunchKernelGGL(k_pieces, dim3(nblk(n)), dim3(kTB), 0, s, n, np, down, prank, q, piece);
+    DDR_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * 8 * (size_t)np, s));
+    hipLaunchKernelGGL(k_piece_table, dim3(nblk(n)), dim3(kTB), 0, s, n, np, down, is_root, piece, dloc, crow, ht, dist,
+                       tab);
+    DDR_HIP(hipGetLastError());
+    htab.resize(8 * (size_t)np);
+    DDR_HIP(hipMemcpyAsync(htab.data(), tab, sizeof(int32_t) * 8 * (size_t)np, hipMemcpyDeviceToHost, s));
+    DDR_HIP(hipStreamSynchronize(s));
+    phase("split");
+    pt = PieceTable{};
+    auto col_of = [&](int c, std::vector<int64_t>& v) { v.assign(htab.begin() + (size_t)c * np, htab.begin() + (size_t)(c + 1) * np); };
+    col_of(0, pt.root);
+    col_of(1, pt.size);
+    col_of(2, pt.dmax);
+    col_of(3, pt.xl);
+    col_of(4, pt.parent);
+    col_of(5, pt.dloc_down);
+    col_of(6, pt.ht_root);
+    col_of(7, pt.dist_root);
+    int outcome = kPackDone;
+    if ((st = pack_pieces(plan, pt, pr, &outcome))) return st;
+    phase("pack");
+    if (outcome == kPackResplit) continue;
+    break;
+  }
+  g->n_pieces = (int64_t)pt.count();
+  if ((st = finalize_blocks(g.get(), plan, pr))) return st;
+  const int64_t nb = pr.nblocks, ncut = pr.ncut, nx_total = g->n_xlist;
+  // ---- persistent arrays (one allocation) ---------------------------------------------------
+  const int64_t words = (n + 1) + e + 4 * n        // crow, col, down, dist, basin, block
+                        + 11 * n + e               // ref off upb upc dloc cut xoff pos_of_ref block_of_pos rs_loc rs_ref, uplist
+                        + 4 * ncut + nx_total;     // v_edge v_off v_dloc cout_loc, xlist
+  const size_t bytes = sizeof(int32_t) * (size_t)words + sizeof(BlockDesc) * (size_t)nb + 64;
+  void* slab = nullptr;
+  DDR_HIP(hipMalloc(&slab, bytes));
+  g->allocations.push_back(slab);
+  int32_t* w = static_cast<int32_t*>(slab);
+  auto carve = [&](int64_t k) {
+    int32_t* p = w;
+    w += k;
+    return p;
+  };
+  DeviceViews& V = g->dviews;
+  V.crow = carve(n + 1);
+  V.col = carve(e);
+  V.down = carve(n);
+  V.dist = carve(n);
+  V.basin = carve(n);
+  V.block = carve(n);
+  DevSchedule& S = g->dev;
+  S.ref = carve(n);
+  S.off = carve(n);
+  S.upb = carve(n);
+  S.upc = carve(n);
+  S.dloc = carve(n);
+  S.cut = carve(n);
+  S.xoff = carve(n);
+  S.pos_of_ref = carve(n);
+  S.block_of_pos = carve(n);
+  S.rs_loc = carve(n);
+  S.rs_ref = carve(n);
+  S.uplist = carve(e);
+  S.v_edge = carve(ncut);
+  S.v_off = carve(ncut);
+  S.v_dloc = carve(ncut);
+  S.cout_loc = carve(ncut);
+  S.xlist = carve(nx_total);
+  {
+    uintptr_t a = reinterpret_cast<uintptr_t>(w);
+    a = (a + 15) & ~uintptr_t(15);
+    S.blocks = reinterpret_cast<BlockDesc*>(a);
+  }
+  DDR_HIP(hipMemcpyAsync(S.blocks, g->blocks.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, s));
+  DDR_HIP(hipMemcpyAsync(V.crow, crow, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s));
+  if (e > 0) DDR_HIP(hipMemcpyAsync(V.col, col, sizeof(int32_t) * e, hipMemcpyDeviceToDevice, s));
+  DDR_HIP(hipMemcpyAsync(V.down, down, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  DDR_HIP(hipMemcpyAsync(V.dist, dist, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  DDR_HIP(hipMemcpyAsync(V.basin, basin, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+  // ---- emission ------------------------------------------------------------------------------
+  int32_t* bop = scr.get<int32_t>((int64_t)pt.count());
+  int32_t* bdmax = scr.get<int32_t>(nb);
+  uint64_t* ekey = scr.get<uint64_t>(n);
+  uint64_t* ekey2 = scr.get<uint64_t>(n);
+  int32_t* offv = scr.get<int32_t>(n);
+  int32_t* order = scr.get<int32_t>(n);
+  int32_t* pos = scr.get<int32_t>(n);
+  int32_t* local = scr.get<int32_t>(n);
+  int32_t* cutf = scr.get<int32_t>(n);
+  int32_t* nv = scr.get<int32_t>(n);
+  int32_t* nx = scr.get<int32_t>(n);
+  int32_t* eid = scr.get<int32_t>(n);
+  int32_t* vbase = scr.get<int32_t>(n);
+  int32_t* xbase = scr.get<int32_t>(n);
+  int32_t* edge_of = scr.get<int32_t>(n);
+  uint32_t* bkey2 = scr.get<uint32_t>(n);
+  DDR_SCR(bop); DDR_SCR(bdmax); DDR_SCR(ekey); DDR_SCR(ekey2); DDR_SCR(offv); DDR_SCR(order); DDR_SCR(pos);
+  DDR_SCR(local); DDR_SCR(cutf); DDR_SCR(nv); DDR_SCR(nx); DDR_SCR(eid); DDR_SCR(vbase); DDR_SCR(xbase);
+  DDR_SCR(edge_of); DDR_SCR(bkey2);
+  std::vector<int32_t> hbop(pr.block_of_piece.begin(), pr.block_of_piece.end());
+  std::vector<int32_t> hbdmax(pr.bdmax.begin(), pr.bdmax.end());
+  int64_t omax = 0;
+  for (int64_t b = 0; b < nb; ++b) omax = std::max<int64_t>(omax, pr.bdmax[b]);
+  DDR_HIP(hipMemcpyAsync(bop, hbop.data(), sizeof(int32_t) * hbop.size(), hipMemcpyHostToDevice, s));
+  DDR_HIP(hipMemcpyAsync(bdmax, hbdmax.data(), sizeof(int32_t) * hbdmax.size(), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_emit_key, dim3(nblk(n)), dim3(kTB), 0, s, n, piece, dloc, bop, bdmax, omax + 1, V.block, offv,
+                     ekey);
+  DDR_HIP(hipGetLastError());
+  if ((st = sort_pairs<uint64_t>(scr, ekey, ekey2, iota, order, n,
+                                 bits_for((uint64_t)(nb - 1) * (uint64_t)(omax + 1) + (uint64_t)omax), s)))
+    return st;
+  hipLaunchKernelGGL(k_emit_counts, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, crow, col, S.blocks, pos,
+                     local, S.upc, cutf, nv, nx, S.pos_of_ref, S.block_of_pos);
+  DDR_HIP(hipGetLastError());
+  if ((st = exclusive_sum<int32_t>(scr, S.upc, S.upb, n, s))) return st;
+  if ((st = exclusive_sum<int32_t>(scr, cutf, eid, n, s))) return st;
+  if ((st = exclusive_sum<int32_t>(scr, nv, vbase, n, s))) return st;
+  if ((st = exclusive_sum<int32_t>(scr, nx, xbase, n, s))) return st;
+  hipLaunchKernelGGL(k_emit_cut, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, local, S.blocks, cutf, eid, nx,
+                     xbase, S.ref, S.off, offv, S.cut, S.cout_loc, edge_of, S.xoff, S.dloc);
+  hipLaunchKernelGGL(k_emit_up, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, crow, col, local, S.blocks, S.upb,
+                     vbase, nx, xbase, offv, edge_of, S.uplist, S.v_edge, S.v_off, S.v_dloc, S.xlist);
+  DDR_HIP(hipGetLastError());
+  // per block, its reaches in ascending reference order (the q' gather's reads): a stable sort by block
+  {
+    const uint32_t* bk = reinterpret_cast<const uint32_t*>(V.block);
+    if ((st = sort_pairs<uint32_t>(scr, bk, bkey2, iota, S.rs_ref, n, bits_for((uint64_t)std::max<int64_t>(nb - 1, 1)),
+                                   s)))
+      return st;
+  }
+  hipLaunchKernelGGL(k_rs_loc, dim3(nblk(n)), dim3(kTB), 0, s, n, S.rs_ref, local, S.rs_loc);
+  DDR_HIP(hipGetLastError());
+  DDR_HIP(hipStreamSynchronize(s));
+  phase("emit");
+  g->uploaded = true;
+  g->device_built = true;
+  *out = g.release();
+  return DDR_OK;
+}
+
+
+ddr_status collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
+                                 const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,
+                                 int64_t* n_active_out, int32_t* rows_c, int32_t* cols_c, int64_t* nnz_out,
+                                 int64_t* crow_out, int32_t* col_out, int64_t* out_off, int32_t* out_idx,
+                                 int64_t out_idx_cap, int32_t* gage_c, hipStream_t s) {
+  if (n_conus <= 0 || n_conus >= (int64_t(1) << 31) - 1) return fail(DDR_ERR_ARG, "bad CONUS size");
+  if (e < 0 || e >= (int64_t(1) << 31) - 1 || (e > 0 && (!rows || !cols))) return fail(DDR_ERR_ARG, "bad subset COO");
+  if (n_gauges < 0 || (n_gauges > 0 && (!gage_idx || !gage_c || !out_idx))) return fail(DDR_ERR_ARG, "bad gauge arrays");
+  if (!active || !n_active_out || !nnz_out || !crow_out || !out_off || (e > 0 && (!rows_c || !cols_c || !col_out)))
+    return fail(DDR_ERR_ARG, "null output");
+  Scratch scr(s);
+  int32_t* down = scr.get<int32_t>(n_conus);
+  int32_t* mark = scr.get<int32_t>(n_conus + 1);
+  int32_t* remap = scr.get<int32_t>(n_conus + 1);
+  unsigned long long* err = scr.get<unsigned long long>(kErrWords);
+  DDR_SCR(down);
+  DDR_SCR(mark);
+  DDR_SCR(remap);
+  DDR_SCR(err);
+  DDR_HIP(hipMemsetAsync(down, 0xFF, sizeof(int32_t) * n_conus, s));
+  DDR_HIP(hipMemsetAsync(mark, 0, sizeof(int32_t) * (n_conus + 1), s));
+  DDR_HIP(hipMemsetAsync(err, 0xFF, sizeof(unsigned long long) * kErrWords, s));
+  if (e > 0) hipLaunchKernelGGL(k_union, dim3(nblk(e)), dim3(kTB), 0, s, n_conus, e, rows, cols, down, mark, err);
+  if (n_gauges > 0)
+    hipLaunchKernelGGL(k_mark_gauges, dim3(nblk(n_gauges)), dim3(kTB), 0, s, n_conus, n_gauges, gage_idx, mark, err);
+  DDR_HIP(hipGetLastError());
+  ddr_status st;
+  if ((st = exclusive_sum<int32_t>(scr, mark, remap, n_conus + 1, s))) return st;
+  unsigned long long herr[kErrWords];
+  int32_t na = 0;
+  DDR_HIP(hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, s));
+  DDR_HIP(hipMemcpyAsync(&na, remap + n_conus, 4, hipMemcpyDeviceToHost, s));
+  DDR_HIP(hipStreamSynchronize(s));
+  const unsigned long long none = ~0ull;
+  if (herr[kErrRange] != none) return fail(DDR_ERR_ARG, "subset COO index or gage_idx out of range");
+  if (herr[kErrLower] != none) {
+    int32_t rc[2];
+    DDR_HIP(hipMemcpy(rc, rows + herr[kErrLower], 4, hipMemcpyDeviceToHost));
+    DDR_HIP(hipMemcpy(rc + 1, cols + herr[kErrLower], 4, hipMemcpyDeviceToHost));
+    return fail(DDR_ERR_NOT_LOWER, "subset entry (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) +
+                                       ") is not strictly lower triangular");
+  }
+  if (herr[kErrDend] != none)
+    return fail(DDR_ERR_NOT_DENDRITIC, "reach " + std::to_string(herr[kErrDend]) +
+                                           " drains into two different reaches in the batch union");
+  if (na > active_cap) return fail(DDR_ERR_ARG, "active reaches exceed active_cap");
+  const int64_t n = na;
+  int32_t* down_c = scr.get<int32_t>(n);
+  int32_t* f = scr.get<int32_t>(n + 1);
+  int32_t* kpos = scr.get<int32_t>(n + 1);
+  int32_t* deg = scr.get<int32_t>(n + 1);
+  int32_t* crow = scr.get<int32_t>(n + 1);
+  DDR_SCR(down_c); DDR_SCR(f); DDR_SCR(kpos); DDR_SCR(deg); DDR_SCR(crow);
+  DDR_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (n + 1), s));
+  DDR_HIP(hipMemsetAsync(f + n, 0, 4, s));
+  hipLaunchKernelGGL(k_compress, dim3(nblk(n_conus)), dim3(kTB), 0, s, n_conus, mark, remap, down, active, down_c);
+  hipLaunchKernelGGL(k_has_down, dim3(nblk(n)), dim3(kTB), 0, s, n, down_c, f, deg);
+  DDR_HIP(hipGetLastError());
+  if ((st = exclusive_sum<int32_t>(scr, f, kpos, n + 1, s))) return st;
+  if ((st = exclusive_sum<int32_t>(scr, deg, crow, n + 1, s))) return st;
+  int32_t nnz = 0;
+  DDR_HIP(hipMemcpyAsync(&nnz, kpos + n, 4, hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(k_union_coo, dim3(nblk(n)), dim3(kTB), 0, s, n, down_c, kpos, rows_c, cols_c);
+  // CSR columns: the compressed reaches sorted by (downstream, index) -- a stable radix sort
+  uint32_t* key = scr.get<uint32_t>(n);
+  uint32_t* key2 = scr.get<uint32_t>(n);
+  int32_t* iota = scr.get<int32_t>(n);
+  int32_t* kids = scr.get<int32_t>(n);
+  DDR_SCR(key); DDR_SCR(key2); DDR_SCR(iota); DDR_SCR(kids);
+  hipLaunchKernelGGL(k_down_key, dim3(nblk(n)), dim3(kTB), 0, s, n, down_c, key);
+  hipLaunchKernelGGL(k_iota, dim3(nblk(n)), dim3(kTB), 0, s, iota, n);
+  DDR_HIP(hipGetLastError());
+  if ((st = sort_pairs<uint32_t>(scr, key, key2, iota, kids, n, bits_for((uint64_t)n), s))) return st;
+  DDR_HIP(hipStreamSynchronize(s));
+  if (nnz > 0) DDR_HIP(hipMemcpyAsync(col_out, kids, sizeof(int32_t) * nnz, hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(k_widen, dim3(nblk(n + 1)), dim3(kTB), 0, s, n + 1, crow, crow_out);
+  if (n_gauges > 0) {
+    int64_t* cnt = scr.get<int64_t>(n_gauges + 1);
+    DDR_SCR(cnt);
+    DDR_HIP(hipMemsetAsync(cnt + n_gauges, 0, 8, s));
+    hipLaunchKernelGGL(k_outflow_count, dim3(nblk(n_gauges)), dim3(kTB), 0, s, n_gauges, gage_idx, remap, crow, gage_c,
+                       cnt);
+    DDR_HIP(hipGetLastError());
+    if ((st = exclusive_sum<int64_t>(scr, cnt, out_off, n_gauges + 1, s))) return st;
+    int64_t total = 0;
+    DDR_HIP(hipMemcpyAsync(&total, out_off + n_gauges, 8, hipMemcpyDeviceToHost, s));
+    DDR_HIP(hipStreamSynchronize(s));
+    if (total > out_idx_cap)
+      return fail(DDR_ERR_ARG, "outflow_idx lists exceed out_idx_cap (" + std::to_string(out_idx_cap) + " entries)");
+    hipLaunchKernelGGL(k_outflow_fill, dim3(nblk(n_gauges)), dim3(kTB), 0, s, n_gauges, gage_c, crow, kids, out_off,
+                       out_idx);
+  } else {
+    DDR_HIP(hipMemsetAsync(out_off, 0, 8, s));
+  }
+  DDR_HIP(hipGetLastError());
+  DDR_HIP(hipStreamSynchronize(s));
+  *n_active_out = n;
+  *nnz_out = nnz;
+  return DDR_OK;
+}
+
+// Host copies of the CSR / structure of a device-built graph (ddr_graph_csr, ddr_graph_structure).
+ddr_status device_views_to_host(const Graph* g, int64_t* crow, int64_t* col, int64_t* down, int64_t* dist,
+                                int64_t* basin, int64_t* block) {
+  const DeviceViews& V = g->dviews;
+  const int64_t n = g->n;
+  std::vector<int32_t> tmp;
+  auto get = [&](const int32_t* src, int64_t k, int64_t* dst) -> ddr_status {
+    if (!dst || k == 0) return DDR_OK;
+    tmp.resize(k);
+    DDR_HIP(hipMemcpy(tmp.data(), src, sizeof(int32_t) * k, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < k; ++i) dst[i] = tmp[i];
+    return DDR_OK;
+  };
+  ddr_status st;
+  if ((st = get(V.crow, n + 1, crow))) return st;
+  if ((st = get(V.col, g->nnz, col))) return st;
+  if ((st = get(V.down, n, down))) return st;
+  if ((st = get(V.dist, n, dist))) return st;
+  if ((st = get(V.basin, n, basin))) return st;
+  if ((st = get(V.block, n, block))) return st;
+  return DDR_OK;
+}
+
+// The schedule arrays of a device-built graph, copied to the host (tests: compared with a host build).
+ddr_status device_schedule_to_host(const Graph* g, HostSchedule& H) {
+  const DevSchedule& S = g->dev;
+  const int64_t n = g->n;
+  auto get = [&](const int32_t* src, int64_t k, std::vector<int32_t>& dst) -> ddr_status {
+    dst.resize(k);
+    if (k) DDR_HIP(hipMemcpy(dst.data(), src, sizeof(int32_t) * k, hipMemcpyDeviceToHost));
+    return DDR_OK;
+  };
+  ddr_status st;
+  if ((st = get(S.ref, n, H.ref)) || (st = get(S.off, n, H.off)) || (st = get(S.upb, n, H.upb)) ||
+      (st = get(S.upc, n, H.upc)) || (st = get(S.dloc, n, H.dloc)) || (st = get(S.cut, n, H.cut)) ||
+      (st = get(S.xoff, n, H.xoff)) || (st = get(S.uplist, g->nnz, H.uplist)) ||
+      (st = get(S.xlist, g->n_xlist, H.xlist)) || (st = get(S.v_edge, g->n_cut, H.v_edge)) ||
+      (st = get(S.v_off, g->n_cut, H.v_off)) || (st = get(S.v_dloc, g->n_cut, H.v_dloc)) ||
+      (st = get(S.cout_loc, g->n_cut, H.cout_loc)) || (st = get(S.pos_of_ref, n, H.pos_of_ref)) ||
+      (st = get(S.block_of_pos, n, H.block_of_pos)) || (st = get(S.rs_loc, n, H.rs_loc)) ||
+      (st = get(S.rs_ref, n, H.rs_ref)))
+    return st;
+  return DDR_OK;
+}
+
+}  // namespace ddr

@@ -120,6 +120,16 @@ struct HostSchedule {
   std::vector<int32_t> pos_of_ref, block_of_pos, rs_loc, rs_ref;
 };
 
+// CSR and structure of a device-built graph (int32, device memory; host copies on request).
+struct DeviceViews {
+  int32_t* crow = nullptr;   // (n + 1)
+  int32_t* col = nullptr;    // (nnz)
+  int32_t* down = nullptr;   // (n)
+  int32_t* dist = nullptr;
+  int32_t* basin = nullptr;
+  int32_t* block = nullptr;
+};
+
 struct Graph {
   int64_t n = 0, nnz = 0;
   std::vector<int64_t> crow, col;
@@ -139,6 +149,8 @@ struct Graph {
   HostSchedule hs;
   DevSchedule dev;
   bool uploaded = false;
+  bool device_built = false;  // built by build_graph_device: crow/col/down/... live in dviews only
+  DeviceViews dviews;
   std::vector<void*> allocations;
 };
 
@@ -200,6 +212,18 @@ ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_
                           const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                           int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
                           int64_t out_idx_cap, int32_t* gage_c);
+// devgraph.hip: the on-device builder (COO in device memory, work on `stream`) and host copies of
+// what it keeps on the device
+ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                              const ddr_build_opts* opts, hipStream_t stream, Graph** out);
+ddr_status collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
+                                 const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,
+                                 int64_t* n_active, int32_t* rows_c, int32_t* cols_c, int64_t* nnz, int64_t* crow,
+                                 int32_t* col, int64_t* out_off, int32_t* out_idx, int64_t out_idx_cap,
+                                 int32_t* gage_c, hipStream_t stream);
+ddr_status device_views_to_host(const Graph* g, int64_t* crow, int64_t* col, int64_t* down, int64_t* dist,
+                                int64_t* basin, int64_t* block);
+ddr_status device_schedule_to_host(const Graph* g, HostSchedule& H);
 // Upload a host-built schedule (DDR_BUILD_HOST_ONLY) to the current device; no-op once uploaded.
 ddr_status upload_schedule(Graph* g);
 

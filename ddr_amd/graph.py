@@ -95,37 +95,72 @@ def _unit_values(vals) -> np.ndarray:
 
 
 class RiverGraph:
-    """Validated, partitioned river network uploaded to the current HIP device."""
+    """Validated, partitioned river network uploaded to the current HIP device.
+
+    ``rows`` / ``cols`` (the COO, row = downstream reach) may be host arrays -- the host builder
+    (``ddr_graph_build``), or ``host_only=True`` for a build that touches no device -- or device
+    tensors, or ``on_device=True``: then the whole build runs on the device (``ddr_graph_build_device``,
+    north star (1)) on ``stream`` (default: the current stream) and the schedule never leaves it.  Both
+    builders emit the same schedule for the same COO (:meth:`fingerprint`)."""
 
     def __init__(self, n: int, rows, cols, *, max_block_reaches: int = 0, target_blocks: int = 0,
-                 max_resident: int = 0, steps_hint: int = 0, host_only: bool = False, device=None):
+                 max_resident: int = 0, steps_hint: int = 0, host_only: bool = False, device=None,
+                 on_device: bool | None = None, stream=None):
         lib = _lib.load()
-        rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
-        cols = np.ascontiguousarray(np.asarray(cols, dtype=np.int32))
-        if rows.shape != cols.shape:
-            raise ValueError("rows and cols must have the same length")
+        import torch
+
+        dev_tensor = isinstance(rows, torch.Tensor) and rows.is_cuda
+        on_device = dev_tensor if on_device is None else bool(on_device)
+        if on_device and host_only:
+            raise ValueError("a device build cannot be host-only")
         opts = _lib.BuildOpts(_lib.DDR_BUILD_HOST_ONLY if host_only else 0, int(max_block_reaches),
                               int(target_blocks), int(max_resident), int(steps_hint))
         handle = C.c_void_p()
         self._handle = None
         self.host_only = host_only
         self.device = None
-        if not host_only:
-            import torch
-
-            dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-            self.device = dev
+        self.device_built = on_device
+        if on_device:
+            if dev_tensor:
+                dev = rows.device
+            else:
+                dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
             with torch.cuda.device(dev):
+                st = stream if stream is not None else torch.cuda.current_stream(dev)
+                with torch.cuda.stream(st):
+                    r = torch.as_tensor(rows).to(dev, torch.int32).contiguous()
+                    c = torch.as_tensor(cols).to(dev, torch.int32).contiguous()
+                if r.shape != c.shape:
+                    raise ValueError("rows and cols must have the same length")
+                # the build synchronises its stream before returning: r and c are no longer in use
+                _lib.check(lib.ddr_graph_build_device(int(n), r.numel(), r.data_ptr(), c.data_ptr(), C.byref(opts),
+                                                      st.cuda_stream, C.byref(handle)))
+            self.device = dev
+        else:
+            rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
+            cols = np.ascontiguousarray(np.asarray(cols, dtype=np.int32))
+            if rows.shape != cols.shape:
+                raise ValueError("rows and cols must have the same length")
+            if not host_only:
+                dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+                self.device = dev
+                with torch.cuda.device(dev):
+                    _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data,
+                                                   C.byref(opts), C.byref(handle)))
+            else:
                 _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data, C.byref(opts),
                                                C.byref(handle)))
-        else:
-            _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data, C.byref(opts),
-                                           C.byref(handle)))
         self._handle = handle
         info = _lib.GraphInfo()
         _lib.check(lib.ddr_graph_get_info(handle, C.byref(info)))
         self.info = GraphInfo(**{f: int(getattr(info, f)) for f, _ in _lib.GraphInfo._fields_})
         self.n = self.info.n
+
+    def fingerprint(self) -> int:
+        """Hash of the whole schedule (equal for a host and a device build of the same COO)."""
+        fp = C.c_uint64()
+        _lib.check(_lib.load().ddr_graph_fingerprint(self._handle, C.byref(fp)))
+        return int(fp.value)
 
     # ------------------------------------------------------------------------------------------
     @classmethod
@@ -241,16 +276,24 @@ class GraphPrefetcher:
     otherwise sit on the critical path of each step.  ``GraphPrefetcher(coo_iter, workers=k)``
     keeps up to ``depth`` builds in flight on ``workers`` threads (the C build releases the GIL) and
     yields uploaded :class:`RiverGraph` objects in order; the upload (~10 ms) runs on the consumer's
-    thread.  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
+    thread.  ``on_device=True`` builds on the device instead (``ddr_graph_build_device``: one builder
+    thread with its own stream; nothing per reach runs on the host).  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
     (e.g. the batch's RoutingDataclass) is returned alongside the graph.  ``upload=False`` yields the
     host-only builds (upload them with :meth:`RiverGraph.upload`).
     """
 
     def __init__(self, coo_iter, *, workers: int = 4, depth: int | None = None, device=None, upload: bool = True,
-                 **build_kw):
+                 on_device: bool = False, **build_kw):
         from concurrent.futures import ThreadPoolExecutor
 
         self._it = iter(coo_iter)
+        self._on_device = bool(on_device)
+        if self._on_device:
+            import torch
+
+            self._dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+            workers = 1  # device builds share the device: one builder thread on its own stream
+            self._stream = torch.cuda.Stream(self._dev)
         self._pool = ThreadPoolExecutor(max_workers=max(1, int(workers)), thread_name_prefix="ddr-graph")
         self._depth = max(1, int(depth if depth is not None else workers + 1))
         self._kw = dict(build_kw)
@@ -261,6 +304,11 @@ class GraphPrefetcher:
 
     def _build(self, item):
         n, rows, cols, *rest = item
+        if self._on_device:
+            # the COO goes up on the builder's stream and the whole build runs there, beside the training
+            # stream; the build synchronises only its own stream
+            g = RiverGraph(n, rows, cols, on_device=True, device=self._dev, stream=self._stream, **self._kw)
+            return g, (rest[0] if rest else None)
         return RiverGraph(n, rows, cols, host_only=True, **self._kw), (rest[0] if rest else None)
 
     def _fill(self):

@@ -11,9 +11,11 @@
  *   ddr_graph_build     src/ddr/geodatazoo/merit.py:197-223 (COO union -> scipy .tocsr())
  *                       + src/ddr/routing/utils.py:25-163 (PatternMapper / get_network_idx)
  *   ddr_graph_upload    (host build on a loader thread, then upload: the per-batch graph of training)
+ *   ddr_graph_build_device  the same build on the device from a device-resident COO (merit.py:197-223,
+ *                       builders.py:55-109 per training batch; north star (1))
  *   ddr_graph_csr       scipy.sparse.coo_matrix(...).tocsr() canonical CSR (bit-exact target)
  *   ddr_collate_gauges  src/ddr/io/builders.py:55-109 construct_network_matrix + merit.py:197-238
- *                       (per-batch gauge union, compression, outflow_idx)
+ *                       (per-batch gauge union, compression, outflow_idx); _device: the same on the device
  *   ddr_mc_forward      src/ddr/routing/mmc.py:365-443 (MuskingumCunge.forward) with
  *                       mmc.py:487-559 (route_timestep), mmc.py:25-66 (compute_hotstart_discharge),
  *                       mmc.py:102-168 + geometry/trapezoidal.py:14-108 (celerity),
@@ -90,6 +92,18 @@ typedef struct {
  * Synchronous (the only host-synchronising call besides ddr_graph_status). */
 ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                            const ddr_build_opts* opts, ddr_graph** out);
+/* The same build from a COO in DEVICE memory (rows / cols: int32 device pointers on the current HIP
+ * device), computed on the device on `stream` (north star (1)): validation, canonical CSR, distance
+ * to outlet, basins, the stem-preserving split and the whole per-workgroup schedule are device
+ * passes; only the packing of the pieces (a few thousand) runs on the host, between two small reads
+ * of the device per split pass.  The schedule equals ddr_graph_build's for the same COO, bit for bit
+ * (ddr_graph_fingerprint).  Returns once the graph is complete on `stream`; its arrays are
+ * device-resident (ddr_graph_csr / ddr_graph_structure copy them to the host on request). */
+ddr_status ddr_graph_build_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                  const ddr_build_opts* opts, void* stream, ddr_graph** out);
+/* FNV-1a hash of a graph's whole schedule (per-reach arrays, block descriptors): equal for a host and
+ * a device build of the same COO and options.  Synchronous (copies the device schedule). */
+ddr_status ddr_graph_fingerprint(const ddr_graph* g, uint64_t* fp);
 /* Per-batch gauge union, replacing construct_network_matrix (src/ddr/io/builders.py:55-109) and the
  * compression steps of Merit._collate_gages (src/ddr/geodatazoo/merit.py:197-238; Lynker twin
  * lynker_hydrofabric.py:198-266).  Host, O(E + n_conus), no device.
@@ -107,6 +121,18 @@ ddr_status ddr_collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* 
                               const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,
                               int64_t* crow, int32_t* col, int64_t* nnz, int64_t* out_off, int32_t* out_idx,
                               int64_t out_idx_cap, int32_t* gage_c);
+/* The same union on the device (all arrays device memory on the current HIP device, work on `stream`):
+ * the subsets concatenated into one COO of e entries (rows / cols, CONUS numbering; the subset
+ * boundaries do not matter to the union).  Outputs: active (active_cap entries) and *n_active (host);
+ * the compressed union as a COO rows_c / cols_c (ascending cols; capacity e) with *nnz (host) entries
+ * -- the input of ddr_graph_build_device -- and as canonical CSR crow (int64, n_active + 1) / col
+ * (capacity e); out_off (int64, n_gauges + 1) / out_idx (out_idx_cap) and gage_c as
+ * ddr_collate_gauges.  Bit-identical to ddr_collate_gauges; synchronous (returns the counts). */
+ddr_status ddr_collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
+                                     const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,
+                                     int64_t* n_active, int32_t* rows_c, int32_t* cols_c, int64_t* nnz, int64_t* crow,
+                                     int32_t* col, int64_t* out_off, int32_t* out_idx, int64_t out_idx_cap,
+                                     int32_t* gage_c, void* stream);
 /* Upload the schedule of a graph built with DDR_BUILD_HOST_ONLY to the current HIP device (no-op
  * if already uploaded).  The host build needs no device: it can run on any host thread (e.g. a
  * data-loader worker preparing the next training batch, merit.py:197-223) while the device routes

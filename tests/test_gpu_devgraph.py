@@ -1,0 +1,181 @@
+"""The on-device graph builder (ddr_graph_build_device, north star (1)): a device-resident COO becomes the
+routing schedule on the device.
+
+Pinned three ways: (1) its schedule equals the host builder's bit for bit (ddr_graph_fingerprint over
+every per-reach array and block descriptor), on shapes from a 5-reach chain to the C5 forest and a
+~1M-reach C3 training batch; (2) its CSR equals SciPy's ``tocsr()`` / the reference's golden CSR
+(merit.py:197-223, ``csr.npz``, ``collate.npz``); (3) a batch collated from the reference's gauge
+subsets (``collate.npz``: builders.py:55-109 + merit.py:197-238) routes through it exactly as the
+oracle.  Invalid networks raise the host builder's error codes.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import PARAMS_DEFAULT, load_golden, maxrel, synthetic_case
+from ddr_amd import _lib, synthetic
+from ddr_amd.graph import RiverGraph
+from oracle import mc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _both(net, **kw):
+    h = RiverGraph(net.n, net.rows, net.cols, **kw)
+    d = RiverGraph(net.n, net.rows, net.cols, on_device=True, **kw)
+    return h, d
+
+
+def _same(h, d):
+    assert d.device_built and not h.device_built
+    assert h.info == d.info, (h.info, d.info)
+    assert h.fingerprint() == d.fingerprint()
+    for a, b in zip(h.csr(), d.csr()):
+        np.testing.assert_array_equal(a, b)
+    sh, sd = h.structure(), d.structure()
+    for k in sh:
+        np.testing.assert_array_equal(sh[k], sd[k], err_msg=k)
+
+
+@pytest.mark.parametrize("kw", [{}, {"max_block_reaches": 128, "target_blocks": 8},
+                                {"max_block_reaches": 400, "target_blocks": 1 << 20}])
+@pytest.mark.parametrize("which", ["chain", "binary300", "hack5000", "forest12k"])
+def test_device_build_equals_host_build(cuda, which, kw):
+    if which == "chain":
+        net = synthetic.SyntheticNetwork(5, np.arange(1, 5, dtype=np.int32), np.arange(0, 4, dtype=np.int32),
+                                         np.array([5]))
+    elif which == "binary300":
+        net = synthetic.random_binary_tree(300, seed=3)
+    elif which == "hack5000":
+        net = synthetic.hack_basin(5000, seed=2)
+    else:
+        net = synthetic.forest(synthetic.loguniform_sizes(40, 20, 2000, 9), seed=9, single_inflow=0.3)
+    h, d = _both(net, **kw)
+    _same(h, d)
+
+
+@pytest.mark.parametrize("which", ["c3_stream_1p07M", "c5"])
+def test_device_build_equals_host_build_full_size(cuda, which):
+    """The builds the benches use: a 1.07M-reach C3 training batch (two generations) and the C5 forest
+    (800k reaches, a 281k-reach basin 2215 deep, split into pieces)."""
+    if which == "c5":
+        net = synthetic.forest(synthetic.zipf_sizes(800_000, 3000, 0.35), seed=5, single_inflow=0.35)
+        T = 8760
+    else:
+        net = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 100), seed=100, single_inflow=0.25)
+        T = 2136
+    h, d = _both(net, steps_hint=T)
+    _same(h, d)
+
+
+def test_device_build_csr_matches_reference_golden(cuda):
+    d = load_golden("csr")
+    for tag, net in (("t300", synthetic.random_binary_tree(300, 3)), ("c1", synthetic.random_binary_tree(2000, 0))):
+        g = RiverGraph(net.n, net.rows, net.cols, on_device=True)
+        crow, col = g.csr()
+        np.testing.assert_array_equal(crow, d[f"{tag}_crow"])
+        np.testing.assert_array_equal(col, d[f"{tag}_col"])
+        mcrow, mcol, src = g.pattern_mapper_layout()
+        np.testing.assert_array_equal(mcrow, d[f"{tag}_mcrow"])
+        np.testing.assert_array_equal(mcol, d[f"{tag}_mcol"])
+        np.testing.assert_array_equal(src, d[f"{tag}_mapidx"])
+
+
+def test_device_build_rejects_invalid_networks(cuda):
+    cases = [
+        (4, [3, 3], [1, 3], _lib.DDR_ERR_NOT_LOWER),       # (3, 3) on the diagonal
+        (4, [1, 3], [0, 2], None),                          # valid: two basins
+        (4, [2, 2], [1, 1], _lib.DDR_ERR_DUPLICATE),
+        (4, [2, 3], [1, 1], _lib.DDR_ERR_NOT_DENDRITIC),   # reach 1 drains into 2 and 3
+        (4, [2, 7], [1, 0], _lib.DDR_ERR_ARG),             # out of range
+    ]
+    for n, r, c, code in cases:
+        rows, cols = np.array(r, np.int32), np.array(c, np.int32)
+        if code is None:
+            RiverGraph(n, rows, cols, on_device=True)
+            continue
+        with pytest.raises(_lib.DDRError) as eh:
+            RiverGraph(n, rows, cols)
+        with pytest.raises(_lib.DDRError) as ed:
+            RiverGraph(n, rows, cols, on_device=True)
+        assert eh.value.code == ed.value.code == code, (r, c, str(ed.value))
+
+
+def test_collated_batch_routes_through_device_graph(cuda):
+    """A training batch collated from the reference's gauge subsets (collate.npz), built on the device:
+    CSR bit-exact with the reference's, gauge-mode discharge equal to the oracle's."""
+    from ddr_amd.batching import collate_gauges
+    from ddr_amd.ops import GaugeMap, RouteConsts, route
+
+    gold = load_golden("collate")
+    off = gold["sub_off"]
+    subs = [(gold["sub_rows"][off[g]:off[g + 1]], gold["sub_cols"][off[g]:off[g + 1]], int(gold["gage_idx"][g]))
+            for g in range(len(off) - 1)]
+    batch = gold["batch"].tolist()
+    keep = [i for i, b in enumerate(gold["gage_ids"].tolist()) if b in batch]
+    cb = collate_gauges(int(gold["n_conus"]), [subs[i] for i in keep])
+    n, rows, cols = cb.coo()
+    g = RiverGraph(n, torch.from_numpy(rows).to(cuda), torch.from_numpy(cols).to(cuda))  # device COO -> device build
+    assert g.device_built
+    crow, col = g.csr()
+    np.testing.assert_array_equal(crow, gold["ref_crow"])
+    np.testing.assert_array_equal(col, gold["ref_col"])
+    T = 72
+    case = synthetic_case(synthetic.SyntheticNetwork(n, rows, cols, np.array([n])), T, 21)
+    r = case.reaches()
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    gz = GaugeMap.build(cb.outflow_idx, n, cuda)
+    out, _, _, _ = route(g, tt(case.qprime), tt(r.n), tt(r.q), tt(r.p), tt(r.length), tt(r.slope), tt(r.x), gauges=gz,
+                         consts=RouteConsts())
+    ref = O.route(case.network(), r, case.qprime, case.bounds, dtype=np.float32, outflow_idx=cb.outflow_idx)
+    assert maxrel(out.cpu().numpy(), ref["runoff"]) <= 1e-6
+    # the same batch through the host build: identical schedule
+    assert RiverGraph(n, rows, cols).fingerprint() == g.fingerprint()
+
+
+def test_device_collate_equals_host_collate(cuda):
+    """The gauge union on the device (ddr_collate_gauges_device) equals the host union, which is pinned
+    to the reference (collate.npz); its compressed COO builds the same graph on the device; bad unions
+    raise the host's codes."""
+    from ddr_amd.batching import collate_gauges, collate_gauges_device
+
+    gold = load_golden("collate")
+    off = gold["sub_off"]
+    subs = [(gold["sub_rows"][off[g]:off[g + 1]], gold["sub_cols"][off[g]:off[g + 1]], int(gold["gage_idx"][g]))
+            for g in range(len(off) - 1)]
+    batch = gold["batch"].tolist()
+    keep = [subs[i] for i, b in enumerate(gold["gage_ids"].tolist()) if b in batch]
+    # a CONUS-scale union as well: 64 nested upstream closures in a 200k-reach forest
+    net = synthetic.forest(synthetic.zipf_sizes(200_000, 400, 0.2), seed=5)
+    down = net.down
+    rng = np.random.default_rng(5)
+    big = []
+    for x in rng.choice(np.flatnonzero(down >= 0), 64, replace=False):
+        inside = np.zeros(net.n, bool)
+        inside[x] = True
+        for j in range(x - 1, max(-1, x - 20000), -1):
+            if down[j] >= 0 and inside[down[j]]:
+                inside[j] = True
+        inside[x] = False
+        ups = np.flatnonzero(inside)
+        big.append((down[ups].astype(np.int32), ups.astype(np.int32), int(x)))
+    for n_conus, ss in ((int(gold["n_conus"]), keep), (net.n, big)):
+        h = collate_gauges(n_conus, ss)
+        d = collate_gauges_device(n_conus, ss, cuda).to_host()
+        np.testing.assert_array_equal(d.active, h.active)
+        np.testing.assert_array_equal(d.crow, h.crow)
+        np.testing.assert_array_equal(d.col, h.col)
+        assert d.gage_compressed_indices == h.gage_compressed_indices
+        for a, b in zip(d.outflow_idx, h.outflow_idx):
+            np.testing.assert_array_equal(a, b)
+        db = collate_gauges_device(n_conus, ss, cuda)
+        g = db.graph()
+        n, rows, cols = h.coo()
+        assert g.device_built and g.fingerprint() == RiverGraph(n, rows, cols).fingerprint()
+    with pytest.raises(_lib.DDRError) as e:
+        collate_gauges_device(5, [(np.array([1]), np.array([0]), 1), (np.array([2]), np.array([0]), 2)], cuda)
+    assert e.value.code == _lib.DDR_ERR_NOT_DENDRITIC
+    with pytest.raises(_lib.DDRError) as e:
+        collate_gauges_device(5, [(np.array([1]), np.array([3]), 1)], cuda)
+    assert e.value.code == _lib.DDR_ERR_NOT_LOWER

@@ -401,3 +401,81 @@ def test_c4_full_size_sampled_basins(cuda):
             assert maxrel(v[ids], orc[k]) <= tol, (b, k)
     del runoff, qp
     torch.cuda.empty_cache()
+
+
+def test_c3_as_benched_daily_store_and_objective(cuda):
+    """The C3 configuration exactly as bench.py runs it (scripts/train.py:54-104): the 896k-reach batch of
+    256 gauged subnetworks over T = 2136 h from a DAILY q' store (89 rows, q'[t // 24], the reader's
+    repeat(24), readers.py:513-519) with missing divides filled with 0.001 (readers.py:523-530), one
+    gauge per subnetwork outlet, the fused daily objective (trim [13 : -11 + tau], area pooling) and the
+    L1 loss over all gauges, backward into n / q / p.
+
+    * exact mode: the daily series of the split 20k-reach basin and of sampled small basins equal the
+      oracle's objective on the same hourly inputs; their parameter gradients equal the fp64 oracle
+      adjoint seeded by the objective's gradient (norm-rel 5e-5);
+    * faithful mode (what the bench times) against exact over the WHOLE batch: daily series within
+      1e-5 max-rel, gradients within the north star's 1e-4 (norm-rel)."""
+    from ddr_amd.ops import DailyWindow
+
+    net = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 3), seed=3, single_inflow=0.25)
+    T, H = T_C3, 24
+    rows = -(-T // H)
+    at = synthetic.reach_attributes(net.n, 11)
+    u = synthetic.unit_parameters(net.n, 11)
+    n, q, p = _physical(u)
+    slope = np.maximum(at.slope, np.float32(1e-3))
+    qd = synthetic.lateral_inflow_torch(net.n, rows, seed=11, device=cuda)
+    valid = np.random.default_rng(12).random(net.n) > 0.02
+    outlets = np.flatnonzero(net.down < 0)
+    G = len(outlets)
+    gz = GaugeMap.build([np.array([o]) for o in outlets], net.n, cuda)
+    w = DailyWindow.for_training(T, 3)
+    wd = 3
+    obs = np.random.default_rng(100).lognormal(np.log(5.0), 1.0, (G, w.D)).astype(np.float32)
+    g = RiverGraph(net.n, net.rows, net.cols, steps_hint=T)
+    assert g.info.generations == 1
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    res = {}
+    for mode in ("exact", "faithful"):
+        nt, qt, pt = (tt(a).requires_grad_(True) for a in (n, q, p))
+        daily, _, _, _ = route(g, qd, nt, qt, pt, tt(at.length), tt(slope), tt(at.x), gauges=gz, daily=w, steps=T,
+                               qprime_hours=H, qprime_valid=tt(valid), consts=RouteConsts(), math=mode)
+        loss = torch.nn.functional.l1_loss(daily[:, wd:], tt(obs)[:, wd:], reduction="sum") / (G * (w.D - wd))
+        loss.backward()
+        torch.cuda.synchronize()
+        res[mode] = (daily.detach().cpu().numpy(), nt.grad.cpu().numpy(), qt.grad.cpu().numpy(), pt.grad.cpu().numpy())
+    ex, fa = res["exact"], res["faithful"]
+    assert maxrel(fa[0], ex[0]) <= 1e-5
+    for a, b in zip(fa[1:], ex[1:]):
+        assert normrel(a, b) <= 1e-4
+    # exact mode vs the oracle on sampled basins (the split 20k basin and four small ones)
+    ff = FullForest.__new__(FullForest)
+    ff.net, ff.graph = net, g
+    members, nblk = _basins_by_blocks(ff)
+    sizes = np.array([len(m) for m in members])
+    big = int(np.argmax(sizes))
+    assert sizes[big] >= 19_000 and nblk[big] >= 2
+    cand = np.flatnonzero((sizes >= 50) & (sizes <= 600))
+    pick = [big] + list(np.random.default_rng(2).choice(cand, size=4, replace=False))
+    ids = np.sort(np.concatenate([members[b] for b in pick]))
+    keep = np.zeros(net.n, bool)
+    keep[ids] = True
+    ns, rs, cs, _ = extract_basins(net.n, net.rows, net.cols, keep)
+    onet = O.Network.from_coo(ns, rs, cs)
+    r = O.Reaches(n[ids], q[ids], p[ids], at.length[ids], slope[ids], at.x[ids])
+    qh = np.repeat(qd[:, torch.from_numpy(ids).to(cuda)].cpu().numpy(), H, axis=0)[:T]
+    qh[:, ~valid[ids]] = np.float32(0.001)
+    loc_out = np.flatnonzero(net.down[ids] < 0)  # the sampled gauges, in global gauge order
+    gsel = np.searchsorted(outlets, ids[loc_out])
+    ref = O.route(onet, r, qh, O.Bounds(), dtype=np.float32, outflow_idx=[np.array([o]) for o in loc_out])
+    _, daily_o, gh = O.daily_l1_objective(ref["runoff"], obs[gsel], 3, wd)
+    assert maxrel(ex[0][gsel], daily_o) <= 1e-6
+    # the global loss's gradient on these gauges: the subset objective's, rescaled from its own mean
+    Wg = np.zeros((ns, T))
+    Wg[loc_out] = gh * (len(gsel) / G)
+    ref64 = O.route(onet, r, qh, O.Bounds(), dtype=np.float64)
+    bw = O.route_backward(onet, r, qh, ref64["x"], Wg, O.Bounds())
+    for a, k in zip(ex[1:], ("n", "q_spatial", "p_spatial")):
+        assert normrel(a[ids], bw[k]) <= 5e-5, k
+    del qd
+    torch.cuda.empty_cache()
