@@ -168,13 +168,24 @@ def cpu_baseline(args, net_global, x_const):
     what = ("fwd (fp32 + SciPy fp64 spsolve_triangular per step) + bwd (hand adjoint + SciPy transposed solve)"
             if grad else "fwd (fp32 + SciPy fp64 spsolve_triangular per step)")
     rs = sample.n * (T - 1)
-    return {"value": rs / el, "unit": "reach-timesteps/s", "cores": 1, "kind": "port",
-            "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s",
-            "forward_only_value": rs / t_fwd,
-            # the reference itself (mmc.py + torch autograd, one core) measured in the build container on
-            # the same kind of trees: the port is a faster stand-in
-            "reference_measured": {"fwd_bwd": 1.3e5, "fwd_only": 3.0e6, "unit": "reach-timesteps/s",
-                                   "source": "BASELINE.md section 2 (2k-100k reaches, 8-core Xeon, 1 core)"}}
+    out = {"value": rs / el, "unit": "reach-timesteps/s", "cores": 1, "nproc": os.cpu_count(), "kind": "port",
+           "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s",
+           "forward_only_value": rs / t_fwd}
+    # the reference itself cannot travel to this box: its speed relative to the port was measured on the
+    # same sample in the build container (tools/calibrate_cpu.py -> profiles/cpu_calibration.json, both on
+    # one core); the reference-equivalent rate here is the port's rate divided by that ratio
+    try:
+        cal = json.loads((ROOT / "profiles" / "cpu_calibration.json").read_text())
+    except (OSError, ValueError):
+        cal = None
+    if cal and w == "c5" and cal.get("reaches") == sample.n and cal.get("T") == T:
+        key = "fwd_bwd" if grad else "fwd_only"
+        ratio = cal["ratio_port_over_reference"][key]
+        out["calibration"] = {"ratio_port_over_reference": ratio, "reference_equivalent_value": out["value" if grad else
+                                                                                                      "forward_only_value"] / ratio,
+                              "reference_in_build_container": cal["reference"][key], "port_in_build_container": cal["port"][key],
+                              "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py, same sample, 1 core)"}
+    return out
 
 
 def counter_file(args, lib_hash):
@@ -212,7 +223,8 @@ def main():
     ap.add_argument("--stream", type=int, default=0,
                     help="C3, 1 GPU: also time K training steps over K different batches (a new gauge-union "
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
-    ap.add_argument("--stream-workers", type=int, default=4, help="host builder threads (--stream-builder host)")
+    ap.add_argument("--stream-workers", type=int, default=4, help="graph builder threads (each device builder on its own stream)")
+    ap.add_argument("--stream-depth", type=int, default=3, help="graphs built ahead of use")
     ap.add_argument("--stream-builder", default="device", choices=["device", "host"],
                     help="where the per-batch graph is built: on the device (ddr_graph_build_device, one builder "
                          "thread on its own stream) or on host threads (ddr_graph_build + upload)")
@@ -268,10 +280,13 @@ def main():
     consts = RouteConsts()
     lib = _lib.load()
     lib_hash = lib.ddr_version().decode().split()[-1]
-    # algorithmic bytes per reach-step: forward q' read + x_save write + runoff write (gauge mode:
-    # no runoff); backward dL/drunoff read + x_save read -- the fp32 adjoint never reads q' (the c4 term of
-    # the VJP folds through the forward identity x = c1 Sx + c2 I + c3 Q + c4 qc, physics.h adjoint_step_fast)
-    fwd_bytes, bwd_bytes = (8, 8) if args.workload == "c3" else (12, 8)
+    # algorithmic bytes per reach-step, SURVEY §8(d): forward q' read + x_save write + runoff write; backward
+    # dL/drunoff read + x_save read + q' read; gauge mode (C3) has no per-reach runoff / dL/drunoff (G x T
+    # only).  These are the roofline's figures.  The fp32 adjoint itself never reads q' (the c4 term of the
+    # VJP folds through the forward identity x = c1 Sx + c2 I + c3 Q + c4 qc, physics.h adjoint_step_fast):
+    # what its kernel moves is 4 B less per reach-step (reported beside it as kernel_bytes_per_reach_step)
+    fwd_bytes, bwd_bytes = (8, 8) if args.workload == "c3" else (12, 12)
+    bwd_kernel_bytes = bwd_bytes - 4
 
     # ---- the step of each workload --------------------------------------------------------------------
     if args.workload == "c5":
@@ -387,7 +402,10 @@ def main():
         for key, nb in (("forward", fwd_bytes), ("backward", bwd_bytes)):
             if kms[key]:
                 k = float(np.mean(kms[key]))
-                kern[key] = {"kernel_ms": k, "GB/s": nb * reach_steps / (k * 1e-3) / 1e9, "bytes_per_reach_step": nb}
+                kern[key] = {"kernel_ms": k, "GB/s": nb * reach_steps / (k * 1e-3) / 1e9, "bytes_per_reach_step": nb,
+                             "launches": len(kms[key])}
+        if "backward" in kern:
+            kern["backward"]["kernel_bytes_per_reach_step"] = bwd_kernel_bytes
         dom = max(kern, key=lambda k_: kern[k_]["kernel_ms"])
         achieved = kern[dom]["GB/s"]
         cf = counter_file(args, lib_hash)
@@ -398,7 +416,9 @@ def main():
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args, net, x_const)
         if cpu is not None:
             cpu["speedup_vs_port"] = value / cpu["value"]
-            cpu["speedup_vs_reference_measured"] = value / cpu["reference_measured"]["fwd_bwd" if spec["grad"] else "fwd_only"]
+            cal = cpu.get("calibration")
+            if cal:
+                cpu["speedup_vs_reference_equivalent"] = value / cal["reference_equivalent_value"]
         largest = int(net.basin_sizes.max())
         out = {
             "metric": spec["metric"],
@@ -427,6 +447,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": kc.get("bytes_per_launch"),
                          "kernel": f"route_{dom}_kernel", "bytes_per_reach_step": kern[dom]["bytes_per_reach_step"],
+                         "bytes_source": "SURVEY.md section 8(d) algorithmic bytes per reach-step x N (T - 1) / the kernel's "
+                                         "mean duration (HIP events on its launch stream)",
                          "valu_frac": kc.get("valu_frac"), "counters": None if cf is None else cf.get("source"),
                          "note": "not HBM bound: VALU issue + per-tick barrier bound, see DESIGN.md section 4"},
             "kernels": kern,
@@ -476,18 +498,26 @@ def time_training_stream(args, dev):
     consts = RouteConsts()
     torch.cuda.synchronize()
     warm = 2
-    on_dev = args.stream_builder == "device"
+    on_dev = args.stream_builder == "device"  # builder threads: --stream-workers (host or device)
     pf = GraphPrefetcher(((data[k % M]["net"].n, data[k % M]["net"].rows, data[k % M]["net"].cols, k % M)
-                          for k in range(K + warm)), workers=args.stream_workers, steps_hint=T, on_device=on_dev)
+                          for k in range(K + warm)), workers=args.stream_workers, steps_hint=T, on_device=on_dev,
+                         depth=args.stream_depth)
     per = []
+    evs = []
     t_start = None
+    g = None
     for k in range(K + warm):
         if k == warm:
             torch.cuda.synchronize()
             t_start = time.perf_counter()
         t0 = time.perf_counter()
+        if g is not None:
+            g.close()  # the previous batch's graph: released stream-ordered after its launches
         g, m = next(pf)
         t_graph = time.perf_counter() - t0
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
         d = data[m]
         opt.zero_grad(set_to_none=True)
         un = model(d["feats"])
@@ -499,16 +529,21 @@ def time_training_stream(args, dev):
         allreduce_gradients(list(model.parameters()))
         torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0, foreach=True)
         opt.step()
+        e1.record()
         if k >= warm:
             per.append({"reaches": int(d["net"].n), "generations": g.info.generations, "blocks": g.info.n_blocks,
                         "graph_wait_ms": round(t_graph * 1e3, 2)})
+            evs.append((e0, e1))
     torch.cuda.synchronize()
     timed = time.perf_counter() - t_start
+    for b, (e0, e1) in zip(per, evs):
+        b["step_gpu_ms"] = round(e0.elapsed_time(e1), 2)
+    g.close()
     pf.close()
     rs = sum(b["reaches"] for b in per) * (T - 1)
     waits = [b["graph_wait_ms"] for b in per]
     return {"steps": K, "ms_per_step": timed / K * 1e3, "value": rs / timed, "unit": "reach-timesteps/s",
-            "graph_builder": args.stream_builder, "graph_workers": 1 if on_dev else args.stream_workers,
+            "graph_builder": args.stream_builder, "graph_workers": args.stream_workers,
             "graph_wait_ms_mean": float(np.mean(waits)) if waits else None, "batches": per,
             "note": (f"new adjacency + graph build per step ({'on the device, builder thread + stream' if on_dev else 'on host threads'}"
                      f", overlapped with training), {M} distinct batches cycled")}

@@ -79,6 +79,7 @@ _SIGS = {
     "ddr_graph_build_device": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P, C.POINTER(C.c_void_p)]),
     "ddr_graph_fingerprint": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "ddr_graph_destroy": (C.c_int, [_P]),
+    "ddr_graph_destroy_async": (C.c_int, [_P, _P]),
     "ddr_graph_upload": (C.c_int, [_P]),
     "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "ddr_collate_gauges_device": (C.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _I64, C.POINTER(C.c_int64), _P, _P,
@@ -94,6 +95,7 @@ _SIGS = {
                                       C.POINTER(Gauges), _P, _P, _P, _P, _P, _I32, _P]),
     "ddr_mc_backward_f64": (C.c_int, [_P, C.POINTER(Consts), C.POINTER(Reaches), _P, _I64, _P, _P, _P,
                                       C.POINTER(Gauges), _P, _P, _P, _P, _P, _I32, _P]),
+    "ddr_hotstart_f32": (C.c_int, [_P, _P, C.c_double, _P, _P]),
     "ddr_state_work_bytes": (_I64, [_P, _I64, _I64, _I32]),
     "ddr_mc_backward_state_f32": (C.c_int, [_P, C.POINTER(Consts), C.POINTER(Reaches), _P, _I64, _I64, _P, _P, _P,
                                             C.POINTER(Gauges), _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P]),

@@ -204,6 +204,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   if ((st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, false))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  DDR_HIP(graph_ready(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bnd, 0xFF, sizeof(double) * g->n_cut * T, s));
   RouteArgs a;
@@ -261,6 +262,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   if ((st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, true))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  DDR_HIP(graph_ready(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
   DDR_HIP(hipMemsetAsync(bwd_bnd + 2 * g->n_cut * T, 0, sizeof(double) * 3 * g->n, s));
@@ -325,6 +327,7 @@ ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   ddr_status st = gauge_args<R>(gh, x_save, T, gz, qlb, flags, a);
   if (st) return st;
   if (!out) return fail(DDR_ERR_ARG, "null gauge output");
+  DDR_HIP(graph_ready(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge<R>(a, x_save, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -343,6 +346,7 @@ ddr_status gauge_daily_impl(const ddr_graph* gh, const R* x_save, int64_t T, con
   if (st) return st;
   if ((st = check_window(T, t0, L, D))) return st;
   if (!out) return fail(DDR_ERR_ARG, "null daily output");
+  DDR_HIP(graph_ready(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge_daily<R>(a, x_save, t0, L, D, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -458,6 +462,13 @@ ddr_status ddr_graph_destroy(ddr_graph* g) {
   })
 }
 
+ddr_status ddr_graph_destroy_async(ddr_graph* g, void* stream) {
+  DDR_GUARD({
+    destroy_graph(reinterpret_cast<Graph*>(g), static_cast<hipStream_t>(stream));
+    return DDR_OK;
+  })
+}
+
 ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
   if (!gh || !info) return fail(DDR_ERR_ARG, "null argument");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
@@ -525,6 +536,38 @@ ddr_status ddr_mc_backward_f64(const ddr_graph* g, const ddr_mc_consts* c, const
                                double* gn, double* gq, double* gp, int32_t flags, void* stream) {
   DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream); })
 }
+ddr_status ddr_hotstart_f32(const ddr_graph* gh, const float* q, double discharge_lb, float* out, void* stream) {
+  DDR_GUARD({
+    if (!gh || !q || !out) return fail(DDR_ERR_ARG, "null hot-start argument");
+    const Graph* g = reinterpret_cast<const Graph*>(gh);
+    if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    // one forward step in accumulation mode (every step a hot start, no coefficient physics): its
+    // workspace is stream-ordered scratch; the per-reach statics are never read for their values
+    const size_t xs = sizeof(float) * 2 * (size_t)(g->n + g->sum_dn);
+    void* ws = nullptr;
+    DDR_HIP(hipMallocAsync(&ws, xs + sizeof(double) * (size_t)std::max<int64_t>(g->n_cut, 1) + kStatusBytes, s));
+    ddr_mc_consts c;
+    c.dt = 3600.0;
+    c.discharge_lb = discharge_lb;
+    c.velocity_lb = 0.01;
+    c.velocity_ub = 15.0;
+    c.depth_lb = 0.01;
+    c.bottom_width_lb = 0.01;
+    c.side_slope_lb = 0.5;
+    c.side_slope_ub = 50.0;
+    ddr_mc_reaches r{};
+    r.n = r.q_spatial = r.p_spatial = r.length = r.slope = r.x_storage = q;
+    r.p_stride = 1;
+    unsigned char* base = static_cast<unsigned char*>(ws);
+    ddr_status st = forward_impl<float>(gh, &c, &r, q, 1, nullptr, out, reinterpret_cast<float*>(base),
+                                        reinterpret_cast<double*>(base + xs), base + xs + sizeof(double) * std::max<int64_t>(g->n_cut, 1),
+                                        nullptr, nullptr, nullptr, DDR_FWD_ACCUMULATE, stream);
+    (void)hipFreeAsync(ws, s);
+    return st;
+  })
+}
+
 int64_t ddr_state_work_bytes(const ddr_graph* g, int64_t T, int64_t n_gauges, int32_t real_bytes) {
   if (!g || T < 1 || n_gauges < 0 || (real_bytes != 4 && real_bytes != 8)) return -1;
   return state_work_bytes(reinterpret_cast<const Graph*>(g), T, n_gauges, (size_t)real_bytes);

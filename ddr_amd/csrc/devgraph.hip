@@ -135,10 +135,11 @@ __global__ void k_is_outlet(int64_t n, const int32_t* down, int32_t* f) {
 }
 
 // Subtree size and height (graph.cpp: sub, ht), one workgroup per basin, deepest level first.
-__global__ void __launch_bounds__(256) k_sub_ht(const int32_t* roots, const int32_t* seg_lo, const int32_t* seg_hi,
-                                                const int32_t* lvl_next, const int32_t* ord, const int32_t* crow,
-                                                const int32_t* col, int32_t* sub, int32_t* ht) {
-  const int32_t root = roots[blockIdx.x];
+__global__ void __launch_bounds__(256) k_sub_ht(const int32_t* roots, const int32_t* nroots, const int32_t* seg_lo,
+                                                const int32_t* seg_hi, const int32_t* lvl_next, const int32_t* ord,
+                                                const int32_t* crow, const int32_t* col, int32_t* sub, int32_t* ht) {
+  for (int32_t b = blockIdx.x; b < *nroots; b += gridDim.x) {
+  const int32_t root = roots[b];
   const int32_t lo = seg_lo[root], hi = seg_hi[root];
   for (int32_t s = lo; s < hi;) {
     const int32_t e = lvl_next[s];
@@ -157,18 +158,23 @@ __global__ void __launch_bounds__(256) k_sub_ht(const int32_t* roots, const int3
     __syncthreads();
     s = e;
   }
+  }
 }
 
 // Stem-preserving split of the basins larger than scap (graph.cpp build_graph, same rule and the
 // same tie-breaks: the deepest child by (height, size), first in column order; the others by
 // ascending residual size, ties in column order).  Smaller basins stay one piece.
-__global__ void __launch_bounds__(256) k_split(const int32_t* roots, const int32_t* seg_lo, const int32_t* seg_hi,
-                                               const int32_t* lvl_next, const int32_t* ord, const int32_t* crow,
-                                               const int32_t* col, const int32_t* sub, const int32_t* ht,
-                                               int32_t* resid, int32_t* stem, uint8_t* is_root, int64_t scap,
-                                               int64_t lseg) {
-  const int32_t root = roots[blockIdx.x];
-  if (sub[root] <= scap) return;
+// scap < 0: the first pass, whose threshold the device chose from the largest basin (k_scap)
+__global__ void __launch_bounds__(256) k_split(const int32_t* roots, const int32_t* nroots, const int32_t* seg_lo,
+                                               const int32_t* seg_hi, const int32_t* lvl_next, const int32_t* ord,
+                                               const int32_t* crow, const int32_t* col, const int32_t* sub,
+                                               const int32_t* ht, int32_t* resid, int32_t* stem, uint8_t* is_root,
+                                               int64_t scap_arg, const int32_t* agg) {
+  const int64_t scap = scap_arg >= 0 ? scap_arg : (int64_t)agg[3];
+  const int64_t lseg = scap / 8;
+  for (int32_t bb = blockIdx.x; bb < *nroots; bb += gridDim.x) {
+  const int32_t root = roots[bb];
+  if (sub[root] <= scap) continue;
   const int32_t lo = seg_lo[root], hi = seg_hi[root];
   for (int32_t s = lo; s < hi;) {
     const int32_t e = lvl_next[s];
@@ -220,6 +226,13 @@ __global__ void __launch_bounds__(256) k_split(const int32_t* roots, const int32
     __syncthreads();
     s = e;
   }
+  }
+}
+// the first pass's split threshold (graph.cpp plan_init: cap x 100 % without a dominant basin, 80 % with
+// one), from the largest basin -- so the host reads the statistics only with the first piece table
+__global__ void k_scap(int64_t n, int64_t cap, int32_t pct_override, int32_t* agg) {
+  const int64_t pct = pct_override > 0 ? pct_override : ((int64_t)agg[2] * 10 < n ? 100 : 80);
+  agg[3] = (int32_t)(cap * pct / 100);
 }
 
 // piece roots: outlets and the reaches the split cut off
@@ -232,28 +245,29 @@ __global__ void k_piece_flags(int64_t n, const int32_t* down, uint8_t* is_root, 
 }
 // piece of every reach (numbered by descending root index: np - 1 - rank of its root) and the piece
 // table (graph.cpp PieceTable); tab is [8][np]
-__global__ void k_pieces(int64_t n, int32_t np, const int32_t* down, const int32_t* prank, const int32_t* q,
+__global__ void k_pieces(int64_t n, const int32_t* np_dev, const int32_t* down, const int32_t* prank, const int32_t* q,
                          int32_t* piece) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) piece[i] = np - 1 - prank[q[i]];
+  if (i < n) piece[i] = *np_dev - 1 - prank[q[i]];
 }
-__global__ void k_piece_table(int64_t n, int32_t np, const int32_t* down, const uint8_t* is_root,
-                              const int32_t* piece, const int32_t* dloc, const int32_t* crow, const int32_t* ht,
-                              const int32_t* dist, int32_t* tab) {
+// column c of piece p at tab[c * n + p]
+__global__ void k_piece_table(int64_t n, const int32_t* down, const uint8_t* is_root, const int32_t* piece,
+                              const int32_t* dloc, const int32_t* crow, const int32_t* ht, const int32_t* dist,
+                              int32_t* tab) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t p = piece[i];
-  atomicAdd(tab + 1 * np + p, 1);
-  atomicMax(tab + 2 * np + p, dloc[i]);
+  atomicAdd(tab + 1 * n + p, 1);
+  atomicMax(tab + 2 * n + p, dloc[i]);
   const int32_t deg = crow[i + 1] - crow[i];
-  if (deg > 2) atomicAdd(tab + 3 * np + p, deg);
+  if (deg > 2) atomicAdd(tab + 3 * n + p, deg);
   if (is_root[i]) {
     const int32_t d = down[i];
-    tab[0 * np + p] = (int32_t)i;
-    tab[4 * np + p] = d < 0 ? -1 : piece[d];
-    tab[5 * np + p] = d < 0 ? 0 : dloc[d];
-    tab[6 * np + p] = ht[i];
-    tab[7 * np + p] = dist[i];
+    tab[0 * n + p] = (int32_t)i;
+    tab[4 * n + p] = d < 0 ? -1 : piece[d];
+    tab[5 * n + p] = d < 0 ? 0 : dloc[d];
+    tab[6 * n + p] = ht[i];
+    tab[7 * n + p] = dist[i];
   }
 }
 
@@ -495,6 +509,20 @@ ddr_status jump(Scratch& scr, int64_t n, const int32_t* down, const uint8_t* sto
   return DDR_OK;
 }
 
+// The default memory pool returns freed memory to the driver at every synchronisation unless told to
+// keep it: a build per training batch would then pay fresh allocations each time.
+void keep_pool_warm() {
+  static bool done = false;
+  if (done) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
+  uint64_t thr = ~0ull;
+  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+  done = true;
+}
+
 int log2_rounds(int64_t len) {
   int r = 1;
   while ((int64_t(1) << (r - 1)) < len + 1) ++r;
@@ -522,6 +550,7 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
     fprintf(stderr, "[dpart] %-10s %8.2f ms\n", what, t - tp);
     tp = t;
   };
+  keep_pool_warm();
   Scratch scr(s);
   // persistent device arrays of the graph: CSR + structure views, then the schedule (one allocation)
   // ---- validation, down[], CSR ----------------------------------------------------------------
@@ -579,42 +608,8 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
   hipLaunchKernelGGL(k_stats, dim3(nblk(n)), dim3(kTB), 0, s, n, down, basin, dist, bsize, agg);
   hipLaunchKernelGGL(k_bmax, dim3(nblk(n)), dim3(kTB), 0, s, n, down, bsize, agg);
   DDR_HIP(hipGetLastError());
-  unsigned long long herr[kErrWords];
-  int32_t hagg[4];
-  DDR_HIP(hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, s));
-  DDR_HIP(hipMemcpyAsync(hagg, agg, sizeof(hagg), hipMemcpyDeviceToHost, s));
-  DDR_HIP(hipStreamSynchronize(s));
   phase("csr+tree");
-  // errors in the host builder's order of precedence (graph.cpp): the first bad entry, then
-  // duplicates, then a reach draining into two reaches
-  {
-    const unsigned long long none = ~0ull;
-    auto entry = [&](unsigned long long k, int32_t* rc) -> ddr_status {
-      DDR_HIP(hipMemcpy(rc, rows + k, 4, hipMemcpyDeviceToHost));
-      DDR_HIP(hipMemcpy(rc + 1, cols + k, 4, hipMemcpyDeviceToHost));
-      return DDR_OK;
-    };
-    int32_t rc[2];
-    if (herr[kErrRange] != none || herr[kErrLower] != none) {
-      if (herr[kErrRange] < herr[kErrLower]) return fail(DDR_ERR_ARG, "COO index out of range");
-      ddr_status st = entry(herr[kErrLower], rc);
-      if (st) return st;
-      return fail(DDR_ERR_NOT_LOWER, "adjacency entry (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) +
-                                         ") is not strictly lower triangular (network not topologically sorted)");
-    }
-    if (herr[kErrDup] != none) {
-      ddr_status st = entry(herr[kErrDup], rc);
-      if (st) return st;
-      return fail(DDR_ERR_DUPLICATE, "duplicate edge (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) + ")");
-    }
-    if (herr[kErrDend] != none)
-      return fail(DDR_ERR_NOT_DENDRITIC, "reach " + std::to_string(herr[kErrDend]) + " drains into two reaches");
-  }
-  const int64_t D = hagg[0];          // deepest reach's distance
-  const int64_t n_basins = hagg[1];
-  const int64_t bmax = hagg[2];
-  g->max_depth = D + 1;
-  g->n_basins = n_basins;
+  // (no host round trip yet: the error words and the statistics are read with the first piece table)
   // ---- level order per basin (deepest level first), subtree size and height --------------------
   uint64_t* lkey = scr.get<uint64_t>(n);
   uint64_t* lkey2 = scr.get<uint64_t>(n);
@@ -626,15 +621,16 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
   int32_t* lvl_next = scr.get<int32_t>(n);
   int32_t* oflag = scr.get<int32_t>(n + 1);
   int32_t* orank = scr.get<int32_t>(n + 1);
-  int32_t* roots = scr.get<int32_t>(n_basins);
+  int32_t* roots = scr.get<int32_t>(n);
   int32_t* sub = scr.get<int32_t>(n);
   int32_t* ht = scr.get<int32_t>(n);
   DDR_SCR(lkey); DDR_SCR(lkey2); DDR_SCR(ord); DDR_SCR(smark); DDR_SCR(smax); DDR_SCR(seg_lo); DDR_SCR(seg_hi);
   DDR_SCR(lvl_next); DDR_SCR(oflag); DDR_SCR(orank); DDR_SCR(roots); DDR_SCR(sub); DDR_SCR(ht);
-  hipLaunchKernelGGL(k_level_key, dim3(nblk(n)), dim3(kTB), 0, s, n, basin, dist, D, lkey);
+  // key = basin * n + (n - 1 - dist): the depth bound n - 1 stands in for the deepest reach (unknown here)
+  hipLaunchKernelGGL(k_level_key, dim3(nblk(n)), dim3(kTB), 0, s, n, basin, dist, n - 1, lkey);
   DDR_HIP(hipGetLastError());
   {
-    ddr_status st = sort_pairs<uint64_t>(scr, lkey, lkey2, iota, ord, n, bits_for((uint64_t)(n - 1) * (uint64_t)(D + 1) + (uint64_t)D), s);
+    ddr_status st = sort_pairs<uint64_t>(scr, lkey, lkey2, iota, ord, n, bits_for((uint64_t)(n - 1) * (uint64_t)n + (uint64_t)(n - 1)), s);
     if (st) return st;
   }
   hipLaunchKernelGGL(k_level_marks, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, ord, basin, smark, seg_lo, seg_hi);
@@ -654,14 +650,25 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
     if (st) return st;
   }
   hipLaunchKernelGGL(k_roots, dim3(nblk(n)), dim3(kTB), 0, s, n, down, orank, roots);
-  hipLaunchKernelGGL(k_sub_ht, dim3((unsigned)n_basins), dim3(256), 0, s, roots, seg_lo, seg_hi, lvl_next, ord, crow,
+  const unsigned basin_grid = (unsigned)std::min<int64_t>(n, 8192);  // workgroups striding over the basins
+  hipLaunchKernelGGL(k_sub_ht, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
                      col, sub, ht);
   DDR_HIP(hipGetLastError());
   phase("sub+ht");
   // ---- split / piece table / host packing, until the packer accepts --------------------------
   PackPlan plan;
-  ddr_status st = plan_init(n, bmax, opts, plan);
+  ddr_status st = plan_init(n, 0, opts, plan);  // the split threshold follows once the largest basin is read
   if (st) return st;
+#ifdef DDR_SCAP_PCT
+  const int32_t pct_override = DDR_SCAP_PCT;
+#else
+  const int32_t pct_override = 0;
+#endif
+  hipLaunchKernelGGL(k_scap, dim3(1), dim3(1), 0, s, n, plan.cap, pct_override, agg);
+  unsigned long long herr[kErrWords];
+  int32_t hagg[4];
+  bool first = true;
+  int64_t D = n - 1;
   g->device = plan.device;
   int32_t* resid = scr.get<int32_t>(n);
   int32_t* stem = scr.get<int32_t>(n);
@@ -677,30 +684,78 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
   PieceTable pt;
   PackResult pr;
   std::vector<int32_t> htab;
+  int64_t prev_np = 0;
   for (;;) {
-    const int64_t scap = plan.scap(), lseg = scap / 8;
     DDR_HIP(hipMemsetAsync(is_root, 0, n, s));
-    hipLaunchKernelGGL(k_split, dim3((unsigned)n_basins), dim3(256), 0, s, roots, seg_lo, seg_hi, lvl_next, ord, crow,
-                       col, sub, ht, resid, stem, is_root, scap, lseg);
+    hipLaunchKernelGGL(k_split, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
+                       col, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
     hipLaunchKernelGGL(k_piece_flags, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, pflag);
     DDR_HIP(hipGetLastError());
     DDR_HIP(hipMemsetAsync(pflag + n, 0, 4, s));  // prank[n] = number of pieces
     if ((st = exclusive_sum<int32_t>(scr, pflag, prank, n + 1, s))) return st;
-    int32_t np = 0;
-    DDR_HIP(hipMemcpyAsync(&np, prank + n, 4, hipMemcpyDeviceToHost, s));
-    if ((st = jump(scr, n, down, is_root, log2_rounds(D + 1), q, dloc, s))) return st;
-    DDR_HIP(hipStreamSynchronize(s));
-    hipLaunchKernelGGL(k_pieces, dim3(nblk(n)), dim3(kTB), 0, s, n, np, down, prank, q, piece);
-    DDR_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * 8 * (size_t)np, s));
-    hipLaunchKernelGGL(k_piece_table, dim3(nblk(n)), dim3(kTB), 0, s, n, np, down, is_root, piece, dloc, crow, ht, dist,
+    if ((st = jump(scr, n, down, is_root, log2_rounds(first ? n : D + 1), q, dloc, s))) return st;
+    // the table is [8][n] (column stride n: no host round trip for the piece count first); one read
+    // of a bounded prefix of every column and of the count, a second one only for very many pieces
+    hipLaunchKernelGGL(k_pieces, dim3(nblk(n)), dim3(kTB), 0, s, n, prank + n, down, prank, q, piece);
+    DDR_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * 8 * (size_t)n, s));
+    hipLaunchKernelGGL(k_piece_table, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, piece, dloc, crow, ht, dist,
                        tab);
     DDR_HIP(hipGetLastError());
-    htab.resize(8 * (size_t)np);
-    DDR_HIP(hipMemcpyAsync(htab.data(), tab, sizeof(int32_t) * 8 * (size_t)np, hipMemcpyDeviceToHost, s));
+    int32_t np = 0;
+    const int64_t guess = std::min<int64_t>(n, std::max<int64_t>(prev_np + prev_np / 4, 16384));
+    htab.resize(8 * (size_t)guess);
+    DDR_HIP(hipMemcpyAsync(&np, prank + n, 4, hipMemcpyDeviceToHost, s));
+    DDR_HIP(hipMemcpy2DAsync(htab.data(), sizeof(int32_t) * guess, tab, sizeof(int32_t) * n, sizeof(int32_t) * guess, 8,
+                             hipMemcpyDeviceToHost, s));
+    if (first) {
+      DDR_HIP(hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, s));
+      DDR_HIP(hipMemcpyAsync(hagg, agg, sizeof(hagg), hipMemcpyDeviceToHost, s));
+    }
     DDR_HIP(hipStreamSynchronize(s));
+    if (first) {
+      // errors in the host builder's order of precedence (graph.cpp): the first bad entry, then
+      // duplicates, then a reach draining into two reaches.  (The passes so far ran on the forest the
+      // valid entries form: no out-of-range access.)
+      const unsigned long long none = ~0ull;
+      auto entry = [&](unsigned long long k, int32_t* rc) -> ddr_status {
+        DDR_HIP(hipMemcpy(rc, rows + k, 4, hipMemcpyDeviceToHost));
+        DDR_HIP(hipMemcpy(rc + 1, cols + k, 4, hipMemcpyDeviceToHost));
+        return DDR_OK;
+      };
+      int32_t rc[2];
+      if (herr[kErrRange] != none || herr[kErrLower] != none) {
+        if (herr[kErrRange] < herr[kErrLower]) return fail(DDR_ERR_ARG, "COO index out of range");
+        if ((st = entry(herr[kErrLower], rc))) return st;
+        return fail(DDR_ERR_NOT_LOWER, "adjacency entry (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) +
+                                           ") is not strictly lower triangular (network not topologically sorted)");
+      }
+      if (herr[kErrDup] != none) {
+        if ((st = entry(herr[kErrDup], rc))) return st;
+        return fail(DDR_ERR_DUPLICATE, "duplicate edge (" + std::to_string(rc[0]) + "," + std::to_string(rc[1]) + ")");
+      }
+      if (herr[kErrDend] != none)
+        return fail(DDR_ERR_NOT_DENDRITIC, "reach " + std::to_string(herr[kErrDend]) + " drains into two reaches");
+      D = hagg[0];  // deepest reach's distance
+      g->max_depth = D + 1;
+      g->n_basins = hagg[1];
+      PackPlan p2;
+      if ((st = plan_init(n, hagg[2], opts, p2))) return st;
+      plan.scap_pct = p2.scap_pct;  // the threshold k_scap chose (same rule)
+      if (plan.scap() != hagg[3]) return fail(DDR_ERR_ARG, "internal: split threshold mismatch");
+      first = false;
+    }
+    if (np > guess) {
+      htab.resize(8 * (size_t)np);
+      DDR_HIP(hipMemcpy2D(htab.data(), sizeof(int32_t) * np, tab, sizeof(int32_t) * n, sizeof(int32_t) * np, 8,
+                          hipMemcpyDeviceToHost));
+    }
+    const int64_t stride = np > guess ? np : guess;  // column pitch of htab
+    prev_np = np;
     phase("split");
     pt = PieceTable{};
-    auto col_of = [&](int c, std::vector<int64_t>& v) { v.assign(htab.begin() + (size_t)c * np, htab.begin() + (size_t)(c + 1) * np); };
+    auto col_of = [&](int c, std::vector<int64_t>& v) {
+      v.assign(htab.begin() + (size_t)c * stride, htab.begin() + (size_t)c * stride + np);
+    };
     col_of(0, pt.root);
     col_of(1, pt.size);
     col_of(2, pt.dmax);
@@ -723,9 +778,11 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
                         + 11 * n + e               // ref off upb upc dloc cut xoff pos_of_ref block_of_pos rs_loc rs_ref, uplist
                         + 4 * ncut + nx_total;     // v_edge v_off v_dloc cout_loc, xlist
   const size_t bytes = sizeof(int32_t) * (size_t)words + sizeof(BlockDesc) * (size_t)nb + 64;
+  // stream-ordered (the default pool, kept warm): freeing a batch's graph (ddr_graph_destroy_async on
+  // the training stream) then needs no device-wide synchronisation, unlike hipFree
   void* slab = nullptr;
-  DDR_HIP(hipMalloc(&slab, bytes));
-  g->allocations.push_back(slab);
+  DDR_HIP(hipMallocAsync(&slab, bytes, s));
+  g->async_allocations.push_back(slab);
   int32_t* w = static_cast<int32_t*>(slab);
   auto carve = [&](int64_t k) {
     int32_t* p = w;
@@ -788,8 +845,11 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
   DDR_SCR(bop); DDR_SCR(bdmax); DDR_SCR(ekey); DDR_SCR(ekey2); DDR_SCR(offv); DDR_SCR(order); DDR_SCR(pos);
   DDR_SCR(local); DDR_SCR(cutf); DDR_SCR(nv); DDR_SCR(nx); DDR_SCR(eid); DDR_SCR(vbase); DDR_SCR(xbase);
   DDR_SCR(edge_of); DDR_SCR(bkey2);
-  std::vector<int32_t> hbop(pr.block_of_piece.begin(), pr.block_of_piece.end());
-  std::vector<int32_t> hbdmax(pr.bdmax.begin(), pr.bdmax.end());
+  // host sources of the asynchronous uploads live as long as the graph
+  std::vector<int32_t>& hbop = g->staging_bop;
+  std::vector<int32_t>& hbdmax = g->staging_bdmax;
+  hbop.assign(pr.block_of_piece.begin(), pr.block_of_piece.end());
+  hbdmax.assign(pr.bdmax.begin(), pr.bdmax.end());
   int64_t omax = 0;
   for (int64_t b = 0; b < nb; ++b) omax = std::max<int64_t>(omax, pr.bdmax[b]);
   DDR_HIP(hipMemcpyAsync(bop, hbop.data(), sizeof(int32_t) * hbop.size(), hipMemcpyHostToDevice, s));
@@ -821,7 +881,10 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
   }
   hipLaunchKernelGGL(k_rs_loc, dim3(nblk(n)), dim3(kTB), 0, s, n, S.rs_ref, local, S.rs_loc);
   DDR_HIP(hipGetLastError());
-  DDR_HIP(hipStreamSynchronize(s));
+  // no final synchronisation: the graph is complete once `ready` fires; every launch that uses it
+  // waits for the event on its own stream first (graph_ready)
+  DDR_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
+  DDR_HIP(hipEventRecord(g->ready, s));
   phase("emit");
   g->uploaded = true;
   g->device_built = true;
@@ -934,6 +997,7 @@ ddr_status collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, c
 // Host copies of the CSR / structure of a device-built graph (ddr_graph_csr, ddr_graph_structure).
 ddr_status device_views_to_host(const Graph* g, int64_t* crow, int64_t* col, int64_t* down, int64_t* dist,
                                 int64_t* basin, int64_t* block) {
+  if (g->ready) DDR_HIP(hipEventSynchronize(g->ready));
   const DeviceViews& V = g->dviews;
   const int64_t n = g->n;
   std::vector<int32_t> tmp;
@@ -956,6 +1020,7 @@ ddr_status device_views_to_host(const Graph* g, int64_t* crow, int64_t* col, int
 
 // The schedule arrays of a device-built graph, copied to the host (tests: compared with a host build).
 ddr_status device_schedule_to_host(const Graph* g, HostSchedule& H) {
+  if (g->ready) DDR_HIP(hipEventSynchronize(g->ready));
   const DevSchedule& S = g->dev;
   const int64_t n = g->n;
   auto get = [&](const int32_t* src, int64_t k, std::vector<int32_t>& dst) -> ddr_status {

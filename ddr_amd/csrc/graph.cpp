@@ -127,6 +127,16 @@ ddr_status plan_init(int64_t n, int64_t bmax, const ddr_build_opts* opts, PackPl
 #endif
   P.weighted = true;
   P.gen = 1;
+  // A network beyond ~97 % of one resident generation (resident x hard_cap reaches: packing never fills
+  // every block) starts at the generation count it needs, instead of reaching it through the failed
+  // one-generation variants (a ~1.07M-reach C3 batch: 1 split pass instead of 4 -- each a device
+  // round trip in the on-device builder)
+  const int64_t per_gen_cap = P.resident * P.hard_cap * 97 / 100;
+  if (n > per_gen_cap) {
+    P.gen = (n + per_gen_cap - 1) / per_gen_cap;
+    const int64_t per_gen = std::min<int64_t>(P.target, P.resident) * P.gen;
+    P.cap = std::min<int64_t>(P.hard_cap, std::max<int64_t>(P.min_cap, (n + per_gen - 1) / per_gen));
+  }
   P.dbg = getenv("DDR_DEBUG_PART") != nullptr;
   return DDR_OK;
 }
@@ -634,9 +644,18 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
   return DDR_OK;
 }
 
-void destroy_graph(Graph* g) {
+// The device builder's memory is freed stream-ordered on `stream` (after the work queued there, e.g. the
+// routing launches that used the graph): no device-wide synchronisation per training batch.  The host
+// builder's arrays (hipMalloc) go through hipFree, which waits for the device.
+void destroy_graph(Graph* g, hipStream_t stream) {
   if (!g) return;
   for (void* p : g->allocations) (void)hipFree(p);
+  if (g->ready) {
+    // the build's last work precedes the free on `stream`
+    (void)hipStreamWaitEvent(stream, g->ready, 0);
+    (void)hipEventDestroy(g->ready);
+  }
+  for (void* p : g->async_allocations) (void)hipFreeAsync(p, stream);
   delete g;
 }
 

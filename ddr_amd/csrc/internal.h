@@ -151,7 +151,10 @@ struct Graph {
   bool uploaded = false;
   bool device_built = false;  // built by build_graph_device: crow/col/down/... live in dviews only
   DeviceViews dviews;
-  std::vector<void*> allocations;
+  hipEvent_t ready = nullptr;  // device builds: recorded on the build stream once the schedule is complete
+  std::vector<int32_t> staging_bop, staging_bdmax;  // host sources of the device build's last uploads
+  std::vector<void*> allocations;        // hipMalloc (host builds)
+  std::vector<void*> async_allocations;  // hipMallocAsync (device builds): freed stream-ordered
 };
 
 // ---- piece-level packing, shared by the host builder (graph.cpp) and the device builder ---------
@@ -206,7 +209,12 @@ const char* last_error_cstr();
 // graph.cpp
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out);
-void destroy_graph(Graph* g);
+void destroy_graph(Graph* g, hipStream_t stream = nullptr);
+// Order `stream` after the device build of `g` (no-op for host builds): every launch that reads the
+// schedule calls this first.
+inline hipError_t graph_ready(const Graph* g, hipStream_t stream) {
+  return g->ready ? hipStreamWaitEvent(stream, g->ready, 0) : hipSuccess;
+}
 // collate.cpp: per-batch gauge union (ddr_collate_gauges)
 ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_off, const int32_t* rows,
                           const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t* n_active,

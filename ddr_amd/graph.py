@@ -132,9 +132,12 @@ class RiverGraph:
                     c = torch.as_tensor(cols).to(dev, torch.int32).contiguous()
                 if r.shape != c.shape:
                     raise ValueError("rows and cols must have the same length")
-                # the build synchronises its stream before returning: r and c are no longer in use
                 _lib.check(lib.ddr_graph_build_device(int(n), r.numel(), r.data_ptr(), c.data_ptr(), C.byref(opts),
                                                       st.cuda_stream, C.byref(handle)))
+                # the build may still be running on `st` (the schedule's last kernels): keep the COO alive
+                # for the caching allocator until then
+                r.record_stream(st)
+                c.record_stream(st)
             self.device = dev
         else:
             rows = np.ascontiguousarray(np.asarray(rows, dtype=np.int32))
@@ -253,7 +256,14 @@ class RiverGraph:
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:
-            _lib.load().ddr_graph_destroy(self._handle)
+            if self.device_built:
+                # stream-ordered release after the work queued on the current stream (the routing launches
+                # that used this graph): no device-wide synchronisation per training batch
+                import torch
+
+                _lib.load().ddr_graph_destroy_async(self._handle, torch.cuda.current_stream(self.device).cuda_stream)
+            else:
+                _lib.load().ddr_graph_destroy(self._handle)
         self._handle = None
 
     def __del__(self):
@@ -276,8 +286,8 @@ class GraphPrefetcher:
     otherwise sit on the critical path of each step.  ``GraphPrefetcher(coo_iter, workers=k)``
     keeps up to ``depth`` builds in flight on ``workers`` threads (the C build releases the GIL) and
     yields uploaded :class:`RiverGraph` objects in order; the upload (~10 ms) runs on the consumer's
-    thread.  ``on_device=True`` builds on the device instead (``ddr_graph_build_device``: one builder
-    thread with its own stream; nothing per reach runs on the host).  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
+    thread.  ``on_device=True`` builds on the device instead (``ddr_graph_build_device``: each builder
+    thread on its own high-priority stream; nothing per reach runs on the host).  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
     (e.g. the batch's RoutingDataclass) is returned alongside the graph.  ``upload=False`` yields the
     host-only builds (upload them with :meth:`RiverGraph.upload`).
     """
@@ -289,11 +299,12 @@ class GraphPrefetcher:
         self._it = iter(coo_iter)
         self._on_device = bool(on_device)
         if self._on_device:
+            import threading
+
             import torch
 
             self._dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-            workers = 1  # device builds share the device: one builder thread on its own stream
-            self._stream = torch.cuda.Stream(self._dev)
+            self._tls = threading.local()  # one build stream per builder thread
         self._pool = ThreadPoolExecutor(max_workers=max(1, int(workers)), thread_name_prefix="ddr-graph")
         self._depth = max(1, int(depth if depth is not None else workers + 1))
         self._kw = dict(build_kw)
@@ -305,9 +316,17 @@ class GraphPrefetcher:
     def _build(self, item):
         n, rows, cols, *rest = item
         if self._on_device:
-            # the COO goes up on the builder's stream and the whole build runs there, beside the training
-            # stream; the build synchronises only its own stream
-            g = RiverGraph(n, rows, cols, on_device=True, device=self._dev, stream=self._stream, **self._kw)
+            # the COO goes up on the builder thread's stream and the whole build runs there, beside the
+            # training stream (high priority: the build's short kernels are dispatched first in the gaps
+            # between the training step's persistent routing launches); the build reads its stream once
+            # per split pass and returns with the schedule still in flight -- routing launches wait for
+            # it on their own stream
+            import torch
+
+            st = getattr(self._tls, "stream", None)
+            if st is None:
+                st = self._tls.stream = torch.cuda.Stream(self._dev, priority=-1)
+            g = RiverGraph(n, rows, cols, on_device=True, device=self._dev, stream=st, **self._kw)
             return g, (rest[0] if rest else None)
         return RiverGraph(n, rows, cols, host_only=True, **self._kw), (rest[0] if rest else None)
 

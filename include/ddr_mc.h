@@ -22,6 +22,7 @@
  *                       mmc.py:460-485 (coefficients), routing/utils.py:535-627 (solver forward)
  *   ddr_mc_backward     torch autograd of the above + routing/utils.py:629-692 (solver backward,
  *                       _backward_cpu 188-242 / _backward_gpu 245-310, _compute_A_gradients 321-389)
+ *   ddr_hotstart_f32    mmc.py:25-66 (compute_hotstart_discharge)
  *   ddr_gauge_reduce    mmc.py:344-363, 405-411, 433-439 (ragged outflow_idx scatter_add)
  *   ddr_tri_solve       routing/utils.py:695 triangular_sparse_solve (general CSR, non-unit diagonal)
  *   ddr_tri_grad_values routing/utils.py:321-389 _compute_A_gradients (gradA = -gradb[row]*x[col])
@@ -141,6 +142,10 @@ ddr_status ddr_graph_upload(ddr_graph* g);
 /* Any graph size builds: workgroups take ticket-ordered logical blocks, so a schedule with more
  * blocks than co-resident workgroups still completes (ddr_graph_info.generations > 1). */
 ddr_status ddr_graph_destroy(ddr_graph* g);
+/* Destroy a graph whose last use is queued on `stream`: a device-built graph's memory is released
+ * stream-ordered (no device-wide synchronisation -- the per-batch graphs of a training loop); a
+ * host-built one's as ddr_graph_destroy. */
+ddr_status ddr_graph_destroy_async(ddr_graph* g, void* stream);
 ddr_status ddr_graph_get_info(const ddr_graph* g, ddr_graph_info* info);
 /* Canonical CSR of the adjacency into host buffers: crow (n+1), col (nnz), int64. */
 ddr_status ddr_graph_csr(const ddr_graph* g, int64_t* crow, int64_t* col);
@@ -225,6 +230,12 @@ ddr_status ddr_mc_forward_f64(const ddr_graph* g, const ddr_mc_consts* c, const 
                               double* x_save, double* bnd, void* status, double* q_last,
                               double* top_width_last, double* side_slope_last, int32_t flags,
                               void* stream);
+
+/* Hot start (src/ddr/routing/mmc.py:25-66 compute_hotstart_discharge): out = max((I - N)^-1 q, lb) for
+ * q (N) in reference order -- the accumulation solve of the routing graph in one launch, fp64 sums as
+ * the reference's SciPy solve; device pointers, enqueued on `stream` (its workspace is stream-ordered
+ * scratch).  The same sweep is step 0 of every ddr_mc_forward_f32 without DDR_FWD_CARRY. */
+ddr_status ddr_hotstart_f32(const ddr_graph* g, const float* q, double discharge_lb, float* out, void* stream);
 
 /* Reverse-time, reverse-topological adjoint.  grad_runoff is (N, T), or (G, T) with gauges != NULL.
  * bwd_bnd is the backward workspace (size in ddr_graph_info).

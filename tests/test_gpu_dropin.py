@@ -102,6 +102,36 @@ def test_hotstart_known_answers(cuda):
         np.testing.assert_array_equal(res.cpu().numpy(), d[f"hot_{name}_out"])
 
 
+def test_hotstart_c_abi_known_answers(cuda):
+    """The C ABI's ddr_hotstart_f32 on the same known answers (tests/routing/test_mmc.py:564-602)
+    and on a 20k-reach forest against the oracle's accumulation solve (fp64 sums, bit-exact)."""
+    import ctypes as C
+
+    from ddr_amd import _lib
+    from ddr_amd.graph import RiverGraph
+    from ddr_amd import synthetic
+    from oracle import mc_oracle as O
+
+    lib = _lib.load()
+    d = load_golden("kat")
+    cases = []
+    for name in ("uniform5", "nonuniform4", "single", "clamp3"):
+        q = d[f"hot_{name}_q"].astype(np.float32)
+        n = len(q)
+        rows, cols = np.arange(1, n, dtype=np.int32), np.arange(0, n - 1, dtype=np.int32)  # a chain
+        cases.append((n, rows, cols, q, float(PARAMS_MOCK["attribute_minimums"]["discharge"]), d[f"hot_{name}_out"]))
+    net = synthetic.forest(synthetic.zipf_sizes(20_000, 60, 0.35), seed=8)
+    q = synthetic.lateral_inflow(net.n, 1, 8)[0]
+    ref = O.hotstart(O.Network.from_coo(net.n, net.rows, net.cols), q, O.Bounds(), np.float32)
+    cases.append((net.n, net.rows, net.cols, q, 1e-4, ref))
+    for n, rows, cols, q, lb, expect in cases:
+        g = RiverGraph(n, rows, cols, max_block_reaches=256, target_blocks=1 << 20)
+        qt = torch.from_numpy(q).to(cuda)
+        out = torch.empty(n, device=cuda)
+        _lib.check(lib.ddr_hotstart_f32(g.handle, qt.data_ptr(), C.c_double(lb), out.data_ptr(), _lib.stream_ptr(cuda)))
+        np.testing.assert_array_equal(out.cpu().numpy(), expect)
+
+
 def test_setup_inputs_semantics(cuda):
     """Slope clamp, hot start, carry_state (test_mmc.py:83-99, 604-636)."""
     mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
