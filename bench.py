@@ -225,7 +225,7 @@ def main():
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
     ap.add_argument("--stream-workers", type=int, default=4, help="graph builder threads (each device builder on its own stream)")
     ap.add_argument("--stream-depth", type=int, default=3, help="graphs built ahead of use")
-    ap.add_argument("--stream-builder", default="device", choices=["device", "host"],
+    ap.add_argument("--stream-builder", default="inline", choices=["inline", "device", "host"],
                     help="where the per-batch graph is built: on the device (ddr_graph_build_device, one builder "
                          "thread on its own stream) or on host threads (ddr_graph_build + upload)")
     ap.add_argument("--fast-math", action="store_true",
@@ -465,6 +465,10 @@ def main():
         dist.destroy_process_group()
 
 
+BUILDERS = {"inline": "on the device, begun ahead on the training stream", "device": "on the device, builder threads",
+            "host": "on host threads + upload"}
+
+
 def time_training_stream(args, dev):
     """C3 as a training loop sees it: every step a new batch of 256 gauged subnetworks, i.e. a new
     adjacency, graph and gauge map per step (merit.py:197-223, scripts/train.py:54-104).  The graph of
@@ -498,7 +502,9 @@ def time_training_stream(args, dev):
     consts = RouteConsts()
     torch.cuda.synchronize()
     warm = 2
-    on_dev = args.stream_builder == "device"  # builder threads: --stream-workers (host or device)
+    # inline: device builds begun --stream-depth batches ahead on the training stream (PendingGraph);
+    # device: device builds on builder threads' own streams; host: host builds on threads + upload
+    on_dev = {"inline": "inline", "device": True, "host": False}[args.stream_builder]
     pf = GraphPrefetcher(((data[k % M]["net"].n, data[k % M]["net"].rows, data[k % M]["net"].cols, k % M)
                           for k in range(K + warm)), workers=args.stream_workers, steps_hint=T, on_device=on_dev,
                          depth=args.stream_depth)
@@ -545,7 +551,7 @@ def time_training_stream(args, dev):
     return {"steps": K, "ms_per_step": timed / K * 1e3, "value": rs / timed, "unit": "reach-timesteps/s",
             "graph_builder": args.stream_builder, "graph_workers": args.stream_workers,
             "graph_wait_ms_mean": float(np.mean(waits)) if waits else None, "batches": per,
-            "note": (f"new adjacency + graph build per step ({'on the device, builder thread + stream' if on_dev else 'on host threads'}"
+            "note": (f"new adjacency + graph build per step ({BUILDERS[args.stream_builder]}"
                      f", overlapped with training), {M} distinct batches cycled")}
 
 

@@ -78,6 +78,10 @@ _SIGS = {
     "ddr_graph_build": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), C.POINTER(C.c_void_p)]),
     "ddr_graph_build_device": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P, C.POINTER(C.c_void_p)]),
     "ddr_graph_fingerprint": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "ddr_graph_build_device_begin": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P,
+                                               C.POINTER(C.c_void_p)]),
+    "ddr_graph_build_device_finish": (C.c_int, [_P, C.POINTER(C.c_void_p)]),
+    "ddr_graph_build_device_cancel": (C.c_int, [_P]),
     "ddr_graph_destroy": (C.c_int, [_P]),
     "ddr_graph_destroy_async": (C.c_int, [_P, _P]),
     "ddr_graph_upload": (C.c_int, [_P]),

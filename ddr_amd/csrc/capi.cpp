@@ -398,6 +398,40 @@ ddr_status ddr_graph_build_device(int64_t n, int64_t e, const int32_t* rows, con
   })
 }
 
+ddr_status ddr_graph_build_device_begin(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                        const ddr_build_opts* opts, void* stream, ddr_graph_pending** out) {
+  DDR_GUARD({
+    if (!out) return fail(DDR_ERR_ARG, "null out");
+    DevBuild* b = nullptr;
+    ddr_status st = build_graph_device_begin(n, e, rows, cols, opts, static_cast<hipStream_t>(stream), &b);
+    if (st) return st;
+    *out = reinterpret_cast<ddr_graph_pending*>(b);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_build_device_finish(ddr_graph_pending* p, ddr_graph** out) {
+  DDR_GUARD({
+    if (!p) return fail(DDR_ERR_ARG, "null pending build");
+    if (!out) {
+      build_graph_device_cancel(reinterpret_cast<DevBuild*>(p));
+      return fail(DDR_ERR_ARG, "null out");
+    }
+    Graph* g = nullptr;
+    ddr_status st = build_graph_device_finish(reinterpret_cast<DevBuild*>(p), &g);
+    if (st) return st;
+    *out = reinterpret_cast<ddr_graph*>(g);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_build_device_cancel(ddr_graph_pending* p) {
+  DDR_GUARD({
+    build_graph_device_cancel(reinterpret_cast<DevBuild*>(p));
+    return DDR_OK;
+  })
+}
+
 ddr_status ddr_graph_fingerprint(const ddr_graph* gh, uint64_t* fp) {
   DDR_GUARD({
     if (!gh || !fp) return fail(DDR_ERR_ARG, "null argument");

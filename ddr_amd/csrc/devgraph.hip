@@ -531,192 +531,223 @@ int log2_rounds(int64_t len) {
 
 }  // namespace
 
-ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
-                              const ddr_build_opts* opts, hipStream_t s, Graph** out) {
-  if (n <= 0) return fail(DDR_ERR_ARG, "graph must have at least one reach");
-  if (n >= (int64_t(1) << 31) - 1 || e >= (int64_t(1) << 31) - 1)
-    return fail(DDR_ERR_ARG, "graph too large for int32 reach ids");
-  if (e < 0 || (e > 0 && (!rows || !cols))) return fail(DDR_ERR_ARG, "bad COO arrays");
-  if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) return fail(DDR_ERR_ARG, "a device build cannot be host-only");
-  auto g = std::make_unique<Graph>();
-  g->n = n;
-  g->nnz = e;
-  const bool dbg = getenv("DDR_DEBUG_PART") != nullptr;
-  double tp = now_ms();
-  auto phase = [&](const char* what) {
+// One device build in two halves (ddr_graph_build_device_begin / _finish): begin() enqueues every
+// device pass up to the first piece table and its copy into pinned host memory, without waiting for
+// anything; finish() waits for that copy (by then long done when the build was begun a training step
+// ahead), packs the pieces on the host, and enqueues the schedule emission.  A re-split (the packer
+// changed the plan: rare, see plan_init) costs one synchronous round trip per extra pass.
+struct DevBuild {
+  int64_t n = 0, e = 0;
+  const int32_t* rows = nullptr;
+  const int32_t* cols = nullptr;
+  ddr_build_opts opts{};
+  bool has_opts = false;
+  hipStream_t s = nullptr;
+  Scratch scr;
+  std::unique_ptr<Graph> g;
+  bool dbg = false, tdbg = false;
+  double t_begin = 0.0, t_pack = 0.0, t_wait = 0.0;
+  // device arrays
+  int32_t *down = nullptr, *deg = nullptr, *agg = nullptr, *crow = nullptr, *iota = nullptr, *kids = nullptr;
+  unsigned long long* err = nullptr;
+  int32_t *basin = nullptr, *dist = nullptr, *ord = nullptr, *seg_lo = nullptr, *seg_hi = nullptr, *lvl_next = nullptr;
+  int32_t *roots = nullptr, *sub = nullptr, *ht = nullptr, *resid = nullptr, *stem = nullptr, *pflag = nullptr;
+  int32_t *prank = nullptr, *q = nullptr, *dloc = nullptr, *piece = nullptr, *tab = nullptr;
+  uint8_t* is_root = nullptr;
+  unsigned basin_grid = 1;
+  // host side of the piece-table reads: pinned, so the copies are truly asynchronous
+  struct Pinned {
+    unsigned long long err[kErrWords];
+    int32_t agg[4];
+    int32_t np;
+  };
+  Pinned* pin = nullptr;
+  int32_t* ptab = nullptr;  // [8][guess] pinned
+  int64_t guess = 0;
+  hipEvent_t tab_ev = nullptr;
+  PackPlan plan;
+  bool first = true;
+  int64_t D = 0, prev_np = 0;
+
+  explicit DevBuild(hipStream_t st) : s(st), scr(st) {}
+  ~DevBuild() {
+    if (tab_ev) (void)hipEventDestroy(tab_ev);
+    if (pin) (void)hipHostFree(pin);
+    if (ptab) (void)hipHostFree(ptab);
+  }
+  const ddr_build_opts* options() const { return has_opts ? &opts : nullptr; }
+
+  void phase(const char* what, double& tp) const {
     if (!dbg) return;
     (void)hipStreamSynchronize(s);
     const double t = now_ms();
     fprintf(stderr, "[dpart] %-10s %8.2f ms\n", what, t - tp);
     tp = t;
-  };
-  keep_pool_warm();
-  Scratch scr(s);
-  // persistent device arrays of the graph: CSR + structure views, then the schedule (one allocation)
-  // ---- validation, down[], CSR ----------------------------------------------------------------
-  int32_t* down = scr.get<int32_t>(n);
-  int32_t* deg = scr.get<int32_t>(n + 1);
-  unsigned long long* err = scr.get<unsigned long long>(kErrWords);
-  int32_t* agg = scr.get<int32_t>(4);
-  DDR_SCR(down);
-  DDR_SCR(deg);
-  DDR_SCR(err);
-  DDR_SCR(agg);
-  DDR_HIP(hipMemsetAsync(down, 0xFF, sizeof(int32_t) * n, s));
-  DDR_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (n + 1), s));
-  DDR_HIP(hipMemsetAsync(err, 0xFF, sizeof(unsigned long long) * kErrWords, s));
-  DDR_HIP(hipMemsetAsync(agg, 0, sizeof(int32_t) * 4, s));
-  if (e > 0) hipLaunchKernelGGL(k_coo, dim3(nblk(e)), dim3(kTB), 0, s, n, e, rows, cols, down, deg, err);
-  DDR_HIP(hipGetLastError());
-  // the persistent slab: crow (n+1), col (e), down, dist, basin, block (n each) + the schedule
-  //   ref, off, upb, upc, dloc, cut, xoff, pos_of_ref, block_of_pos, rs_loc, rs_ref (n each),
-  //   uplist (e); v_edge, v_off, v_dloc, cout_loc (<= e each); xlist (<= e + n); blocks (later)
-  int32_t* crow = scr.get<int32_t>(n + 1);
-  DDR_SCR(crow);
-  {
-    ddr_status st = exclusive_sum<int32_t>(scr, deg, crow, n + 1, s);
-    if (st) return st;
   }
-  uint32_t* dkey = scr.get<uint32_t>(n);
-  uint32_t* dkey2 = scr.get<uint32_t>(n);
-  int32_t* iota = scr.get<int32_t>(n);
-  int32_t* kids = scr.get<int32_t>(n);  // reaches sorted by (downstream, index): the CSR's col
-  DDR_SCR(dkey);
-  DDR_SCR(dkey2);
-  DDR_SCR(iota);
-  DDR_SCR(kids);
-  hipLaunchKernelGGL(k_down_key, dim3(nblk(n)), dim3(kTB), 0, s, n, down, dkey);
-  hipLaunchKernelGGL(k_iota, dim3(nblk(n)), dim3(kTB), 0, s, iota, n);
-  DDR_HIP(hipGetLastError());
-  {
-    ddr_status st = sort_pairs<uint32_t>(scr, dkey, dkey2, iota, kids, n, bits_for((uint64_t)n), s);
-    if (st) return st;
-  }
-  const int32_t* col = kids;  // first e entries
-  // ---- distance to outlet, basin ------------------------------------------------------------
-  int32_t* basin = scr.get<int32_t>(n);
-  int32_t* dist = scr.get<int32_t>(n);
-  DDR_SCR(basin);
-  DDR_SCR(dist);
-  {
-    ddr_status st = jump(scr, n, down, nullptr, log2_rounds(n), basin, dist, s);
-    if (st) return st;
-  }
-  int32_t* bsize = scr.get<int32_t>(n);
-  DDR_SCR(bsize);
-  DDR_HIP(hipMemsetAsync(bsize, 0, sizeof(int32_t) * n, s));
-  hipLaunchKernelGGL(k_stats, dim3(nblk(n)), dim3(kTB), 0, s, n, down, basin, dist, bsize, agg);
-  hipLaunchKernelGGL(k_bmax, dim3(nblk(n)), dim3(kTB), 0, s, n, down, bsize, agg);
-  DDR_HIP(hipGetLastError());
-  phase("csr+tree");
-  // (no host round trip yet: the error words and the statistics are read with the first piece table)
-  // ---- level order per basin (deepest level first), subtree size and height --------------------
-  uint64_t* lkey = scr.get<uint64_t>(n);
-  uint64_t* lkey2 = scr.get<uint64_t>(n);
-  int32_t* ord = scr.get<int32_t>(n);
-  int32_t* smark = scr.get<int32_t>(n);
-  int32_t* smax = scr.get<int32_t>(n);
-  int32_t* seg_lo = scr.get<int32_t>(n);
-  int32_t* seg_hi = scr.get<int32_t>(n);
-  int32_t* lvl_next = scr.get<int32_t>(n);
-  int32_t* oflag = scr.get<int32_t>(n + 1);
-  int32_t* orank = scr.get<int32_t>(n + 1);
-  int32_t* roots = scr.get<int32_t>(n);
-  int32_t* sub = scr.get<int32_t>(n);
-  int32_t* ht = scr.get<int32_t>(n);
-  DDR_SCR(lkey); DDR_SCR(lkey2); DDR_SCR(ord); DDR_SCR(smark); DDR_SCR(smax); DDR_SCR(seg_lo); DDR_SCR(seg_hi);
-  DDR_SCR(lvl_next); DDR_SCR(oflag); DDR_SCR(orank); DDR_SCR(roots); DDR_SCR(sub); DDR_SCR(ht);
-  // key = basin * n + (n - 1 - dist): the depth bound n - 1 stands in for the deepest reach (unknown here)
-  hipLaunchKernelGGL(k_level_key, dim3(nblk(n)), dim3(kTB), 0, s, n, basin, dist, n - 1, lkey);
-  DDR_HIP(hipGetLastError());
-  {
-    ddr_status st = sort_pairs<uint64_t>(scr, lkey, lkey2, iota, ord, n, bits_for((uint64_t)(n - 1) * (uint64_t)n + (uint64_t)(n - 1)), s);
-    if (st) return st;
-  }
-  hipLaunchKernelGGL(k_level_marks, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, ord, basin, smark, seg_lo, seg_hi);
-  DDR_HIP(hipGetLastError());
-  {
-    size_t bytes = 0;
-    DDR_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, bytes, smark, smax, hipcub::Max(), (int)n, s));
-    void* tmp = scr.get<unsigned char>((int64_t)bytes);
-    DDR_SCR(tmp);
-    DDR_HIP(hipcub::DeviceScan::InclusiveScan(tmp, bytes, smark, smax, hipcub::Max(), (int)n, s));
-  }
-  hipLaunchKernelGGL(k_level_links, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, smax, lvl_next);
-  hipLaunchKernelGGL(k_is_outlet, dim3(nblk(n)), dim3(kTB), 0, s, n, down, oflag);
-  DDR_HIP(hipGetLastError());
-  {
-    ddr_status st = exclusive_sum<int32_t>(scr, oflag, orank, n, s);
-    if (st) return st;
-  }
-  hipLaunchKernelGGL(k_roots, dim3(nblk(n)), dim3(kTB), 0, s, n, down, orank, roots);
-  const unsigned basin_grid = (unsigned)std::min<int64_t>(n, 8192);  // workgroups striding over the basins
-  hipLaunchKernelGGL(k_sub_ht, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
-                     col, sub, ht);
-  DDR_HIP(hipGetLastError());
-  phase("sub+ht");
-  // ---- split / piece table / host packing, until the packer accepts --------------------------
-  PackPlan plan;
-  ddr_status st = plan_init(n, 0, opts, plan);  // the split threshold follows once the largest basin is read
-  if (st) return st;
+
+  ddr_status begin() {
+    g = std::make_unique<Graph>();
+    g->n = n;
+    g->nnz = e;
+    double tp = now_ms();
+    keep_pool_warm();
+    // ---- validation, down[], CSR --------------------------------------------------------------
+    down = scr.get<int32_t>(n);
+    deg = scr.get<int32_t>(n + 1);
+    err = scr.get<unsigned long long>(kErrWords);
+    agg = scr.get<int32_t>(4);
+    DDR_SCR(down);
+    DDR_SCR(deg);
+    DDR_SCR(err);
+    DDR_SCR(agg);
+    DDR_HIP(hipMemsetAsync(down, 0xFF, sizeof(int32_t) * n, s));
+    DDR_HIP(hipMemsetAsync(deg, 0, sizeof(int32_t) * (n + 1), s));
+    DDR_HIP(hipMemsetAsync(err, 0xFF, sizeof(unsigned long long) * kErrWords, s));
+    DDR_HIP(hipMemsetAsync(agg, 0, sizeof(int32_t) * 4, s));
+    if (e > 0) hipLaunchKernelGGL(k_coo, dim3(nblk(e)), dim3(kTB), 0, s, n, e, rows, cols, down, deg, err);
+    DDR_HIP(hipGetLastError());
+    crow = scr.get<int32_t>(n + 1);
+    DDR_SCR(crow);
+    ddr_status st;
+    if ((st = exclusive_sum<int32_t>(scr, deg, crow, n + 1, s))) return st;
+    uint32_t* dkey = scr.get<uint32_t>(n);
+    uint32_t* dkey2 = scr.get<uint32_t>(n);
+    iota = scr.get<int32_t>(n);
+    kids = scr.get<int32_t>(n);  // reaches sorted by (downstream, index): the CSR's col
+    DDR_SCR(dkey);
+    DDR_SCR(dkey2);
+    DDR_SCR(iota);
+    DDR_SCR(kids);
+    hipLaunchKernelGGL(k_down_key, dim3(nblk(n)), dim3(kTB), 0, s, n, down, dkey);
+    hipLaunchKernelGGL(k_iota, dim3(nblk(n)), dim3(kTB), 0, s, iota, n);
+    DDR_HIP(hipGetLastError());
+    if ((st = sort_pairs<uint32_t>(scr, dkey, dkey2, iota, kids, n, bits_for((uint64_t)n), s))) return st;
+    // ---- distance to outlet, basin --------------------------------------------------------------
+    basin = scr.get<int32_t>(n);
+    dist = scr.get<int32_t>(n);
+    DDR_SCR(basin);
+    DDR_SCR(dist);
+    if ((st = jump(scr, n, down, nullptr, log2_rounds(n), basin, dist, s))) return st;
+    int32_t* bsize = scr.get<int32_t>(n);
+    DDR_SCR(bsize);
+    DDR_HIP(hipMemsetAsync(bsize, 0, sizeof(int32_t) * n, s));
+    hipLaunchKernelGGL(k_stats, dim3(nblk(n)), dim3(kTB), 0, s, n, down, basin, dist, bsize, agg);
+    hipLaunchKernelGGL(k_bmax, dim3(nblk(n)), dim3(kTB), 0, s, n, down, bsize, agg);
+    DDR_HIP(hipGetLastError());
+    phase("csr+tree", tp);
+    // (no host round trip yet: the error words and the statistics are read with the first piece table)
+    // ---- level order per basin (deepest level first), subtree size and height ------------------
+    uint64_t* lkey = scr.get<uint64_t>(n);
+    uint64_t* lkey2 = scr.get<uint64_t>(n);
+    ord = scr.get<int32_t>(n);
+    int32_t* smark = scr.get<int32_t>(n);
+    int32_t* smax = scr.get<int32_t>(n);
+    seg_lo = scr.get<int32_t>(n);
+    seg_hi = scr.get<int32_t>(n);
+    lvl_next = scr.get<int32_t>(n);
+    int32_t* oflag = scr.get<int32_t>(n + 1);
+    int32_t* orank = scr.get<int32_t>(n + 1);
+    roots = scr.get<int32_t>(n);
+    sub = scr.get<int32_t>(n);
+    ht = scr.get<int32_t>(n);
+    DDR_SCR(lkey); DDR_SCR(lkey2); DDR_SCR(ord); DDR_SCR(smark); DDR_SCR(smax); DDR_SCR(seg_lo); DDR_SCR(seg_hi);
+    DDR_SCR(lvl_next); DDR_SCR(oflag); DDR_SCR(orank); DDR_SCR(roots); DDR_SCR(sub); DDR_SCR(ht);
+    // key = basin * n + (n - 1 - dist): the depth bound n - 1 stands in for the deepest reach (unknown here)
+    hipLaunchKernelGGL(k_level_key, dim3(nblk(n)), dim3(kTB), 0, s, n, basin, dist, n - 1, lkey);
+    DDR_HIP(hipGetLastError());
+    if ((st = sort_pairs<uint64_t>(scr, lkey, lkey2, iota, ord, n,
+                                   bits_for((uint64_t)(n - 1) * (uint64_t)n + (uint64_t)(n - 1)), s)))
+      return st;
+    hipLaunchKernelGGL(k_level_marks, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, ord, basin, smark, seg_lo, seg_hi);
+    DDR_HIP(hipGetLastError());
+    {
+      size_t bytes = 0;
+      DDR_HIP(hipcub::DeviceScan::InclusiveScan(nullptr, bytes, smark, smax, hipcub::Max(), (int)n, s));
+      void* tmp = scr.get<unsigned char>((int64_t)bytes);
+      DDR_SCR(tmp);
+      DDR_HIP(hipcub::DeviceScan::InclusiveScan(tmp, bytes, smark, smax, hipcub::Max(), (int)n, s));
+    }
+    hipLaunchKernelGGL(k_level_links, dim3(nblk(n)), dim3(kTB), 0, s, n, lkey2, smax, lvl_next);
+    hipLaunchKernelGGL(k_is_outlet, dim3(nblk(n)), dim3(kTB), 0, s, n, down, oflag);
+    DDR_HIP(hipGetLastError());
+    if ((st = exclusive_sum<int32_t>(scr, oflag, orank, n, s))) return st;
+    hipLaunchKernelGGL(k_roots, dim3(nblk(n)), dim3(kTB), 0, s, n, down, orank, roots);
+    basin_grid = (unsigned)std::min<int64_t>(n, 8192);  // workgroups striding over the basins
+    hipLaunchKernelGGL(k_sub_ht, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
+                       kids, sub, ht);
+    DDR_HIP(hipGetLastError());
+    phase("sub+ht", tp);
+    // ---- the first split pass (its threshold chosen on the device from the largest basin) -----
+    if ((st = plan_init(n, 0, options(), plan))) return st;
 #ifdef DDR_SCAP_PCT
-  const int32_t pct_override = DDR_SCAP_PCT;
+    const int32_t pct_override = DDR_SCAP_PCT;
 #else
-  const int32_t pct_override = 0;
+    const int32_t pct_override = 0;
 #endif
-  hipLaunchKernelGGL(k_scap, dim3(1), dim3(1), 0, s, n, plan.cap, pct_override, agg);
-  unsigned long long herr[kErrWords];
-  int32_t hagg[4];
-  bool first = true;
-  int64_t D = n - 1;
-  g->device = plan.device;
-  int32_t* resid = scr.get<int32_t>(n);
-  int32_t* stem = scr.get<int32_t>(n);
-  uint8_t* is_root = scr.get<uint8_t>(n);
-  int32_t* pflag = scr.get<int32_t>(n + 1);
-  int32_t* prank = scr.get<int32_t>(n + 1);
-  int32_t* q = scr.get<int32_t>(n);
-  int32_t* dloc = scr.get<int32_t>(n);
-  int32_t* piece = scr.get<int32_t>(n);
-  int32_t* tab = scr.get<int32_t>(8 * n);
-  DDR_SCR(resid); DDR_SCR(stem); DDR_SCR(is_root); DDR_SCR(pflag); DDR_SCR(prank); DDR_SCR(q); DDR_SCR(dloc);
-  DDR_SCR(piece); DDR_SCR(tab);
-  PieceTable pt;
-  PackResult pr;
-  std::vector<int32_t> htab;
-  int64_t prev_np = 0;
-  for (;;) {
+    hipLaunchKernelGGL(k_scap, dim3(1), dim3(1), 0, s, n, plan.cap, pct_override, agg);
+    g->device = plan.device;
+    resid = scr.get<int32_t>(n);
+    stem = scr.get<int32_t>(n);
+    is_root = scr.get<uint8_t>(n);
+    pflag = scr.get<int32_t>(n + 1);
+    prank = scr.get<int32_t>(n + 1);
+    q = scr.get<int32_t>(n);
+    dloc = scr.get<int32_t>(n);
+    piece = scr.get<int32_t>(n);
+    tab = scr.get<int32_t>(8 * n);
+    DDR_SCR(resid); DDR_SCR(stem); DDR_SCR(is_root); DDR_SCR(pflag); DDR_SCR(prank); DDR_SCR(q); DDR_SCR(dloc);
+    DDR_SCR(piece); DDR_SCR(tab);
+    DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&pin), sizeof(Pinned), hipHostMallocDefault));
+    guess = std::min<int64_t>(n, 16384);
+    DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ptab), sizeof(int32_t) * 8 * (size_t)guess, hipHostMallocDefault));
+    DDR_HIP(hipEventCreateWithFlags(&tab_ev, hipEventDisableTiming));
+    D = n - 1;
+    return pass();
+  }
+
+  // Enqueue one split pass with the current plan and the read of its piece table.
+  ddr_status pass() {
+    ddr_status st;
     DDR_HIP(hipMemsetAsync(is_root, 0, n, s));
     hipLaunchKernelGGL(k_split, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
-                       col, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
+                       kids, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
     hipLaunchKernelGGL(k_piece_flags, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, pflag);
     DDR_HIP(hipGetLastError());
     DDR_HIP(hipMemsetAsync(pflag + n, 0, 4, s));  // prank[n] = number of pieces
     if ((st = exclusive_sum<int32_t>(scr, pflag, prank, n + 1, s))) return st;
     if ((st = jump(scr, n, down, is_root, log2_rounds(first ? n : D + 1), q, dloc, s))) return st;
-    // the table is [8][n] (column stride n: no host round trip for the piece count first); one read
-    // of a bounded prefix of every column and of the count, a second one only for very many pieces
+    // the table is [8][n] (column stride n: no host round trip for the piece count first); a bounded
+    // prefix of every column and the count go to pinned memory, a second read only for many pieces
     hipLaunchKernelGGL(k_pieces, dim3(nblk(n)), dim3(kTB), 0, s, n, prank + n, down, prank, q, piece);
     DDR_HIP(hipMemsetAsync(tab, 0, sizeof(int32_t) * 8 * (size_t)n, s));
     hipLaunchKernelGGL(k_piece_table, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, piece, dloc, crow, ht, dist,
                        tab);
     DDR_HIP(hipGetLastError());
-    int32_t np = 0;
-    const int64_t guess = std::min<int64_t>(n, std::max<int64_t>(prev_np + prev_np / 4, 16384));
-    htab.resize(8 * (size_t)guess);
-    DDR_HIP(hipMemcpyAsync(&np, prank + n, 4, hipMemcpyDeviceToHost, s));
-    DDR_HIP(hipMemcpy2DAsync(htab.data(), sizeof(int32_t) * guess, tab, sizeof(int32_t) * n, sizeof(int32_t) * guess, 8,
+    DDR_HIP(hipMemcpyAsync(&pin->np, prank + n, 4, hipMemcpyDeviceToHost, s));
+    DDR_HIP(hipMemcpy2DAsync(ptab, sizeof(int32_t) * guess, tab, sizeof(int32_t) * n, sizeof(int32_t) * guess, 8,
                              hipMemcpyDeviceToHost, s));
     if (first) {
-      DDR_HIP(hipMemcpyAsync(herr, err, sizeof(herr), hipMemcpyDeviceToHost, s));
-      DDR_HIP(hipMemcpyAsync(hagg, agg, sizeof(hagg), hipMemcpyDeviceToHost, s));
+      DDR_HIP(hipMemcpyAsync(pin->err, err, sizeof(pin->err), hipMemcpyDeviceToHost, s));
+      DDR_HIP(hipMemcpyAsync(pin->agg, agg, sizeof(pin->agg), hipMemcpyDeviceToHost, s));
     }
-    DDR_HIP(hipStreamSynchronize(s));
+    DDR_HIP(hipEventRecord(tab_ev, s));
+    return DDR_OK;
+  }
+
+  // Wait for the pass's table; validation errors and statistics on the first one.
+  ddr_status read_table(PieceTable& pt) {
+    ddr_status st;
+    {
+      const double t0 = now_ms();
+      DDR_HIP(hipEventSynchronize(tab_ev));
+      t_wait += now_ms() - t0;
+    }
     if (first) {
       // errors in the host builder's order of precedence (graph.cpp): the first bad entry, then
       // duplicates, then a reach draining into two reaches.  (The passes so far ran on the forest the
       // valid entries form: no out-of-range access.)
       const unsigned long long none = ~0ull;
+      const unsigned long long* herr = pin->err;
       auto entry = [&](unsigned long long k, int32_t* rc) -> ddr_status {
         DDR_HIP(hipMemcpy(rc, rows + k, 4, hipMemcpyDeviceToHost));
         DDR_HIP(hipMemcpy(rc + 1, cols + k, 4, hipMemcpyDeviceToHost));
@@ -735,27 +766,29 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
       }
       if (herr[kErrDend] != none)
         return fail(DDR_ERR_NOT_DENDRITIC, "reach " + std::to_string(herr[kErrDend]) + " drains into two reaches");
-      D = hagg[0];  // deepest reach's distance
+      D = pin->agg[0];  // deepest reach's distance
       g->max_depth = D + 1;
-      g->n_basins = hagg[1];
+      g->n_basins = pin->agg[1];
       PackPlan p2;
-      if ((st = plan_init(n, hagg[2], opts, p2))) return st;
+      if ((st = plan_init(n, pin->agg[2], options(), p2))) return st;
       plan.scap_pct = p2.scap_pct;  // the threshold k_scap chose (same rule)
-      if (plan.scap() != hagg[3]) return fail(DDR_ERR_ARG, "internal: split threshold mismatch");
+      if (plan.scap() != pin->agg[3]) return fail(DDR_ERR_ARG, "internal: split threshold mismatch");
       first = false;
     }
+    const int64_t np = pin->np;
+    std::vector<int32_t> big;
+    const int32_t* src = ptab;
+    int64_t stride = guess;
     if (np > guess) {
-      htab.resize(8 * (size_t)np);
-      DDR_HIP(hipMemcpy2D(htab.data(), sizeof(int32_t) * np, tab, sizeof(int32_t) * n, sizeof(int32_t) * np, 8,
+      big.resize(8 * (size_t)np);
+      DDR_HIP(hipMemcpy2D(big.data(), sizeof(int32_t) * np, tab, sizeof(int32_t) * n, sizeof(int32_t) * np, 8,
                           hipMemcpyDeviceToHost));
+      src = big.data();
+      stride = np;
     }
-    const int64_t stride = np > guess ? np : guess;  // column pitch of htab
     prev_np = np;
-    phase("split");
     pt = PieceTable{};
-    auto col_of = [&](int c, std::vector<int64_t>& v) {
-      v.assign(htab.begin() + (size_t)c * stride, htab.begin() + (size_t)c * stride + np);
-    };
+    auto col_of = [&](int c, std::vector<int64_t>& v) { v.assign(src + (size_t)c * stride, src + (size_t)c * stride + np); };
     col_of(0, pt.root);
     col_of(1, pt.size);
     col_of(2, pt.dmax);
@@ -764,134 +797,197 @@ ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const i
     col_of(5, pt.dloc_down);
     col_of(6, pt.ht_root);
     col_of(7, pt.dist_root);
-    int outcome = kPackDone;
-    if ((st = pack_pieces(plan, pt, pr, &outcome))) return st;
-    phase("pack");
-    if (outcome == kPackResplit) continue;
-    break;
+    return DDR_OK;
   }
-  g->n_pieces = (int64_t)pt.count();
-  if ((st = finalize_blocks(g.get(), plan, pr))) return st;
-  const int64_t nb = pr.nblocks, ncut = pr.ncut, nx_total = g->n_xlist;
-  // ---- persistent arrays (one allocation) ---------------------------------------------------
-  const int64_t words = (n + 1) + e + 4 * n        // crow, col, down, dist, basin, block
-                        + 11 * n + e               // ref off upb upc dloc cut xoff pos_of_ref block_of_pos rs_loc rs_ref, uplist
-                        + 4 * ncut + nx_total;     // v_edge v_off v_dloc cout_loc, xlist
-  const size_t bytes = sizeof(int32_t) * (size_t)words + sizeof(BlockDesc) * (size_t)nb + 64;
-  // stream-ordered (the default pool, kept warm): freeing a batch's graph (ddr_graph_destroy_async on
-  // the training stream) then needs no device-wide synchronisation, unlike hipFree
-  void* slab = nullptr;
-  DDR_HIP(hipMallocAsync(&slab, bytes, s));
-  g->async_allocations.push_back(slab);
-  int32_t* w = static_cast<int32_t*>(slab);
-  auto carve = [&](int64_t k) {
-    int32_t* p = w;
-    w += k;
-    return p;
-  };
-  DeviceViews& V = g->dviews;
-  V.crow = carve(n + 1);
-  V.col = carve(e);
-  V.down = carve(n);
-  V.dist = carve(n);
-  V.basin = carve(n);
-  V.block = carve(n);
-  DevSchedule& S = g->dev;
-  S.ref = carve(n);
-  S.off = carve(n);
-  S.upb = carve(n);
-  S.upc = carve(n);
-  S.dloc = carve(n);
-  S.cut = carve(n);
-  S.xoff = carve(n);
-  S.pos_of_ref = carve(n);
-  S.block_of_pos = carve(n);
-  S.rs_loc = carve(n);
-  S.rs_ref = carve(n);
-  S.uplist = carve(e);
-  S.v_edge = carve(ncut);
-  S.v_off = carve(ncut);
-  S.v_dloc = carve(ncut);
-  S.cout_loc = carve(ncut);
-  S.xlist = carve(nx_total);
-  {
-    uintptr_t a = reinterpret_cast<uintptr_t>(w);
-    a = (a + 15) & ~uintptr_t(15);
-    S.blocks = reinterpret_cast<BlockDesc*>(a);
-  }
-  DDR_HIP(hipMemcpyAsync(S.blocks, g->blocks.data(), sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, s));
-  DDR_HIP(hipMemcpyAsync(V.crow, crow, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s));
-  if (e > 0) DDR_HIP(hipMemcpyAsync(V.col, col, sizeof(int32_t) * e, hipMemcpyDeviceToDevice, s));
-  DDR_HIP(hipMemcpyAsync(V.down, down, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
-  DDR_HIP(hipMemcpyAsync(V.dist, dist, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
-  DDR_HIP(hipMemcpyAsync(V.basin, basin, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
-  // ---- emission ------------------------------------------------------------------------------
-  int32_t* bop = scr.get<int32_t>((int64_t)pt.count());
-  int32_t* bdmax = scr.get<int32_t>(nb);
-  uint64_t* ekey = scr.get<uint64_t>(n);
-  uint64_t* ekey2 = scr.get<uint64_t>(n);
-  int32_t* offv = scr.get<int32_t>(n);
-  int32_t* order = scr.get<int32_t>(n);
-  int32_t* pos = scr.get<int32_t>(n);
-  int32_t* local = scr.get<int32_t>(n);
-  int32_t* cutf = scr.get<int32_t>(n);
-  int32_t* nv = scr.get<int32_t>(n);
-  int32_t* nx = scr.get<int32_t>(n);
-  int32_t* eid = scr.get<int32_t>(n);
-  int32_t* vbase = scr.get<int32_t>(n);
-  int32_t* xbase = scr.get<int32_t>(n);
-  int32_t* edge_of = scr.get<int32_t>(n);
-  uint32_t* bkey2 = scr.get<uint32_t>(n);
-  DDR_SCR(bop); DDR_SCR(bdmax); DDR_SCR(ekey); DDR_SCR(ekey2); DDR_SCR(offv); DDR_SCR(order); DDR_SCR(pos);
-  DDR_SCR(local); DDR_SCR(cutf); DDR_SCR(nv); DDR_SCR(nx); DDR_SCR(eid); DDR_SCR(vbase); DDR_SCR(xbase);
-  DDR_SCR(edge_of); DDR_SCR(bkey2);
-  // host sources of the asynchronous uploads live as long as the graph
-  std::vector<int32_t>& hbop = g->staging_bop;
-  std::vector<int32_t>& hbdmax = g->staging_bdmax;
-  hbop.assign(pr.block_of_piece.begin(), pr.block_of_piece.end());
-  hbdmax.assign(pr.bdmax.begin(), pr.bdmax.end());
-  int64_t omax = 0;
-  for (int64_t b = 0; b < nb; ++b) omax = std::max<int64_t>(omax, pr.bdmax[b]);
-  DDR_HIP(hipMemcpyAsync(bop, hbop.data(), sizeof(int32_t) * hbop.size(), hipMemcpyHostToDevice, s));
-  DDR_HIP(hipMemcpyAsync(bdmax, hbdmax.data(), sizeof(int32_t) * hbdmax.size(), hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_emit_key, dim3(nblk(n)), dim3(kTB), 0, s, n, piece, dloc, bop, bdmax, omax + 1, V.block, offv,
-                     ekey);
-  DDR_HIP(hipGetLastError());
-  if ((st = sort_pairs<uint64_t>(scr, ekey, ekey2, iota, order, n,
-                                 bits_for((uint64_t)(nb - 1) * (uint64_t)(omax + 1) + (uint64_t)omax), s)))
-    return st;
-  hipLaunchKernelGGL(k_emit_counts, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, crow, col, S.blocks, pos,
-                     local, S.upc, cutf, nv, nx, S.pos_of_ref, S.block_of_pos);
-  DDR_HIP(hipGetLastError());
-  if ((st = exclusive_sum<int32_t>(scr, S.upc, S.upb, n, s))) return st;
-  if ((st = exclusive_sum<int32_t>(scr, cutf, eid, n, s))) return st;
-  if ((st = exclusive_sum<int32_t>(scr, nv, vbase, n, s))) return st;
-  if ((st = exclusive_sum<int32_t>(scr, nx, xbase, n, s))) return st;
-  hipLaunchKernelGGL(k_emit_cut, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, local, S.blocks, cutf, eid, nx,
-                     xbase, S.ref, S.off, offv, S.cut, S.cout_loc, edge_of, S.xoff, S.dloc);
-  hipLaunchKernelGGL(k_emit_up, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, crow, col, local, S.blocks, S.upb,
-                     vbase, nx, xbase, offv, edge_of, S.uplist, S.v_edge, S.v_off, S.v_dloc, S.xlist);
-  DDR_HIP(hipGetLastError());
-  // per block, its reaches in ascending reference order (the q' gather's reads): a stable sort by block
-  {
-    const uint32_t* bk = reinterpret_cast<const uint32_t*>(V.block);
-    if ((st = sort_pairs<uint32_t>(scr, bk, bkey2, iota, S.rs_ref, n, bits_for((uint64_t)std::max<int64_t>(nb - 1, 1)),
-                                   s)))
+
+  ddr_status finish(Graph** out) {
+    double tp = now_ms();
+    ddr_status st;
+    PieceTable pt;
+    PackResult pr;
+    for (;;) {
+      if ((st = read_table(pt))) return st;
+      phase("split", tp);
+      int outcome = kPackDone;
+      const double tpk = now_ms();
+      if ((st = pack_pieces(plan, pt, pr, &outcome))) return st;
+      t_pack += now_ms() - tpk;
+      phase("pack", tp);
+      if (outcome == kPackDone) break;
+      if ((st = pass())) return st;  // a re-split: its table is waited for at the top of the loop
+    }
+    g->n_pieces = (int64_t)pt.count();
+    if ((st = finalize_blocks(g.get(), plan, pr))) return st;
+    const int64_t nb = pr.nblocks, ncut = pr.ncut, nx_total = g->n_xlist;
+    const int32_t* col = kids;
+    // ---- persistent arrays (one allocation) -------------------------------------------------
+    const int64_t words = (n + 1) + e + 4 * n        // crow, col, down, dist, basin, block
+                          + 11 * n + e               // ref off upb upc dloc cut xoff pos_of_ref block_of_pos rs_loc rs_ref, uplist
+                          + 4 * ncut + nx_total;     // v_edge v_off v_dloc cout_loc, xlist
+    const size_t bytes = sizeof(int32_t) * (size_t)words + sizeof(BlockDesc) * (size_t)nb + 64;
+    // stream-ordered (the default pool, kept warm): freeing a batch's graph (ddr_graph_destroy_async on
+    // the training stream) then needs no device-wide synchronisation, unlike hipFree
+    void* slab = nullptr;
+    DDR_HIP(hipMallocAsync(&slab, bytes, s));
+    g->async_allocations.push_back(slab);
+    int32_t* w = static_cast<int32_t*>(slab);
+    auto carve = [&](int64_t k) {
+      int32_t* p = w;
+      w += k;
+      return p;
+    };
+    DeviceViews& V = g->dviews;
+    V.crow = carve(n + 1);
+    V.col = carve(e);
+    V.down = carve(n);
+    V.dist = carve(n);
+    V.basin = carve(n);
+    V.block = carve(n);
+    DevSchedule& S = g->dev;
+    S.ref = carve(n);
+    S.off = carve(n);
+    S.upb = carve(n);
+    S.upc = carve(n);
+    S.dloc = carve(n);
+    S.cut = carve(n);
+    S.xoff = carve(n);
+    S.pos_of_ref = carve(n);
+    S.block_of_pos = carve(n);
+    S.rs_loc = carve(n);
+    S.rs_ref = carve(n);
+    S.uplist = carve(e);
+    S.v_edge = carve(ncut);
+    S.v_off = carve(ncut);
+    S.v_dloc = carve(ncut);
+    S.cout_loc = carve(ncut);
+    S.xlist = carve(nx_total);
+    {
+      uintptr_t a = reinterpret_cast<uintptr_t>(w);
+      a = (a + 15) & ~uintptr_t(15);
+      S.blocks = reinterpret_cast<BlockDesc*>(a);
+    }
+    // host sources of the asynchronous uploads live as long as the graph (pinned: truly asynchronous)
+    const size_t nstage = sizeof(BlockDesc) * (size_t)nb + sizeof(int32_t) * ((size_t)pt.count() + (size_t)nb);
+    DDR_HIP(hipHostMalloc(&g->staging, std::max<size_t>(nstage, 16), hipHostMallocDefault));
+    BlockDesc* hblk = static_cast<BlockDesc*>(g->staging);
+    std::copy(g->blocks.begin(), g->blocks.end(), hblk);
+    int32_t* hbop = reinterpret_cast<int32_t*>(hblk + nb);
+    int32_t* hbdmax = hbop + pt.count();
+    for (size_t p = 0; p < pt.count(); ++p) hbop[p] = (int32_t)pr.block_of_piece[p];
+    int64_t omax = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+      hbdmax[b] = (int32_t)pr.bdmax[b];
+      omax = std::max<int64_t>(omax, pr.bdmax[b]);
+    }
+    DDR_HIP(hipMemcpyAsync(S.blocks, hblk, sizeof(BlockDesc) * nb, hipMemcpyHostToDevice, s));
+    DDR_HIP(hipMemcpyAsync(V.crow, crow, sizeof(int32_t) * (n + 1), hipMemcpyDeviceToDevice, s));
+    if (e > 0) DDR_HIP(hipMemcpyAsync(V.col, col, sizeof(int32_t) * e, hipMemcpyDeviceToDevice, s));
+    DDR_HIP(hipMemcpyAsync(V.down, down, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+    DDR_HIP(hipMemcpyAsync(V.dist, dist, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+    DDR_HIP(hipMemcpyAsync(V.basin, basin, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, s));
+    // ---- emission ------------------------------------------------------------------------------
+    int32_t* bop = scr.get<int32_t>((int64_t)pt.count());
+    int32_t* bdmax = scr.get<int32_t>(nb);
+    uint64_t* ekey = scr.get<uint64_t>(n);
+    uint64_t* ekey2 = scr.get<uint64_t>(n);
+    int32_t* offv = scr.get<int32_t>(n);
+    int32_t* order = scr.get<int32_t>(n);
+    int32_t* pos = scr.get<int32_t>(n);
+    int32_t* local = scr.get<int32_t>(n);
+    int32_t* cutf = scr.get<int32_t>(n);
+    int32_t* nv = scr.get<int32_t>(n);
+    int32_t* nx = scr.get<int32_t>(n);
+    int32_t* eid = scr.get<int32_t>(n);
+    int32_t* vbase = scr.get<int32_t>(n);
+    int32_t* xbase = scr.get<int32_t>(n);
+    int32_t* edge_of = scr.get<int32_t>(n);
+    uint32_t* bkey2 = scr.get<uint32_t>(n);
+    DDR_SCR(bop); DDR_SCR(bdmax); DDR_SCR(ekey); DDR_SCR(ekey2); DDR_SCR(offv); DDR_SCR(order); DDR_SCR(pos);
+    DDR_SCR(local); DDR_SCR(cutf); DDR_SCR(nv); DDR_SCR(nx); DDR_SCR(eid); DDR_SCR(vbase); DDR_SCR(xbase);
+    DDR_SCR(edge_of); DDR_SCR(bkey2);
+    DDR_HIP(hipMemcpyAsync(bop, hbop, sizeof(int32_t) * pt.count(), hipMemcpyHostToDevice, s));
+    DDR_HIP(hipMemcpyAsync(bdmax, hbdmax, sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_emit_key, dim3(nblk(n)), dim3(kTB), 0, s, n, piece, dloc, bop, bdmax, omax + 1, V.block, offv,
+                       ekey);
+    DDR_HIP(hipGetLastError());
+    if ((st = sort_pairs<uint64_t>(scr, ekey, ekey2, iota, order, n,
+                                   bits_for((uint64_t)(nb - 1) * (uint64_t)(omax + 1) + (uint64_t)omax), s)))
       return st;
+    hipLaunchKernelGGL(k_emit_counts, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, crow, col, S.blocks, pos,
+                       local, S.upc, cutf, nv, nx, S.pos_of_ref, S.block_of_pos);
+    DDR_HIP(hipGetLastError());
+    if ((st = exclusive_sum<int32_t>(scr, S.upc, S.upb, n, s))) return st;
+    if ((st = exclusive_sum<int32_t>(scr, cutf, eid, n, s))) return st;
+    if ((st = exclusive_sum<int32_t>(scr, nv, vbase, n, s))) return st;
+    if ((st = exclusive_sum<int32_t>(scr, nx, xbase, n, s))) return st;
+    hipLaunchKernelGGL(k_emit_cut, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, down, local, S.blocks, cutf, eid,
+                       nx, xbase, S.ref, S.off, offv, S.cut, S.cout_loc, edge_of, S.xoff, S.dloc);
+    hipLaunchKernelGGL(k_emit_up, dim3(nblk(n)), dim3(kTB), 0, s, n, order, V.block, crow, col, local, S.blocks, S.upb,
+                       vbase, nx, xbase, offv, edge_of, S.uplist, S.v_edge, S.v_off, S.v_dloc, S.xlist);
+    DDR_HIP(hipGetLastError());
+    // per block, its reaches in ascending reference order (the q' gather's reads): a stable sort by block
+    {
+      const uint32_t* bk = reinterpret_cast<const uint32_t*>(V.block);
+      if ((st = sort_pairs<uint32_t>(scr, bk, bkey2, iota, S.rs_ref, n,
+                                     bits_for((uint64_t)std::max<int64_t>(nb - 1, 1)), s)))
+        return st;
+    }
+    hipLaunchKernelGGL(k_rs_loc, dim3(nblk(n)), dim3(kTB), 0, s, n, S.rs_ref, local, S.rs_loc);
+    DDR_HIP(hipGetLastError());
+    // no final synchronisation: the graph is complete once `ready` fires; every launch that uses it
+    // waits for the event on its own stream first (graph_ready)
+    DDR_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
+    DDR_HIP(hipEventRecord(g->ready, s));
+    phase("emit", tp);
+    if (tdbg)
+      fprintf(stderr, "[devbuild] n %ld begin->finish %.2f ms, waited %.2f ms, pack %.2f ms, blocks %ld gen %ld\n",
+              (long)n, now_ms() - t_begin, t_wait, t_pack, (long)nb, (long)g->generations);
+    g->uploaded = true;
+    g->device_built = true;
+    *out = g.release();
+    return DDR_OK;
   }
-  hipLaunchKernelGGL(k_rs_loc, dim3(nblk(n)), dim3(kTB), 0, s, n, S.rs_ref, local, S.rs_loc);
-  DDR_HIP(hipGetLastError());
-  // no final synchronisation: the graph is complete once `ready` fires; every launch that uses it
-  // waits for the event on its own stream first (graph_ready)
-  DDR_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
-  DDR_HIP(hipEventRecord(g->ready, s));
-  phase("emit");
-  g->uploaded = true;
-  g->device_built = true;
-  *out = g.release();
+};
+
+ddr_status build_graph_device_begin(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                    const ddr_build_opts* opts, hipStream_t s, DevBuild** out) {
+  if (n <= 0) return fail(DDR_ERR_ARG, "graph must have at least one reach");
+  if (n >= (int64_t(1) << 31) - 1 || e >= (int64_t(1) << 31) - 1)
+    return fail(DDR_ERR_ARG, "graph too large for int32 reach ids");
+  if (e < 0 || (e > 0 && (!rows || !cols))) return fail(DDR_ERR_ARG, "bad COO arrays");
+  if (opts && (opts->flags & DDR_BUILD_HOST_ONLY)) return fail(DDR_ERR_ARG, "a device build cannot be host-only");
+  auto b = std::make_unique<DevBuild>(s);
+  b->n = n;
+  b->e = e;
+  b->rows = rows;
+  b->cols = cols;
+  if (opts) {
+    b->opts = *opts;
+    b->has_opts = true;
+  }
+  b->dbg = getenv("DDR_DEBUG_PART") != nullptr;
+  b->tdbg = getenv("DDR_DEBUG_BUILD_TIMING") != nullptr;
+  b->t_begin = now_ms();
+  ddr_status st = b->begin();
+  if (st) return st;
+  *out = b.release();
   return DDR_OK;
 }
 
+ddr_status build_graph_device_finish(DevBuild* b, Graph** out) {
+  std::unique_ptr<DevBuild> own(b);
+  return b->finish(out);
+}
+
+void build_graph_device_cancel(DevBuild* b) { delete b; }
+
+ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                              const ddr_build_opts* opts, hipStream_t s, Graph** out) {
+  DevBuild* b = nullptr;
+  ddr_status st = build_graph_device_begin(n, e, rows, cols, opts, s, &b);
+  if (st) return st;
+  return build_graph_device_finish(b, out);
+}
 
 ddr_status collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
                                  const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,

@@ -650,12 +650,14 @@ ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t*
 void destroy_graph(Graph* g, hipStream_t stream) {
   if (!g) return;
   for (void* p : g->allocations) (void)hipFree(p);
-  if (g->ready) {
-    // the build's last work precedes the free on `stream`
-    (void)hipStreamWaitEvent(stream, g->ready, 0);
-    (void)hipEventDestroy(g->ready);
-  }
+  if (g->ready) (void)hipStreamWaitEvent(stream, g->ready, 0);  // the build's last work precedes the free
   for (void* p : g->async_allocations) (void)hipFreeAsync(p, stream);
+  if (g->staging) {
+    // the build's uploads read it: long complete by the time a graph is released
+    if (g->ready) (void)hipEventSynchronize(g->ready);
+    (void)hipHostFree(g->staging);
+  }
+  if (g->ready) (void)hipEventDestroy(g->ready);
   delete g;
 }
 

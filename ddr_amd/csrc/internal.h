@@ -152,7 +152,7 @@ struct Graph {
   bool device_built = false;  // built by build_graph_device: crow/col/down/... live in dviews only
   DeviceViews dviews;
   hipEvent_t ready = nullptr;  // device builds: recorded on the build stream once the schedule is complete
-  std::vector<int32_t> staging_bop, staging_bdmax;  // host sources of the device build's last uploads
+  void* staging = nullptr;     // pinned host sources of the device build's last uploads
   std::vector<void*> allocations;        // hipMalloc (host builds)
   std::vector<void*> async_allocations;  // hipMallocAsync (device builds): freed stream-ordered
 };
@@ -224,6 +224,11 @@ ddr_status collate_gauges(int64_t n_conus, int64_t n_gauges, const int64_t* sub_
 // what it keeps on the device
 ddr_status build_graph_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                               const ddr_build_opts* opts, hipStream_t stream, Graph** out);
+struct DevBuild;  // a device build between its two halves
+ddr_status build_graph_device_begin(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                    const ddr_build_opts* opts, hipStream_t stream, DevBuild** out);
+ddr_status build_graph_device_finish(DevBuild* b, Graph** out);  // consumes b
+void build_graph_device_cancel(DevBuild* b);
 ddr_status collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t e, const int32_t* rows,
                                  const int32_t* cols, const int32_t* gage_idx, int32_t* active, int64_t active_cap,
                                  int64_t* n_active, int32_t* rows_c, int32_t* cols_c, int64_t* nnz, int64_t* crow,

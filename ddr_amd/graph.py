@@ -159,6 +159,20 @@ class RiverGraph:
         self.info = GraphInfo(**{f: int(getattr(info, f)) for f, _ in _lib.GraphInfo._fields_})
         self.n = self.info.n
 
+    @classmethod
+    def _adopt(cls, handle: C.c_void_p, device, device_built: bool) -> "RiverGraph":
+        """Wrap a finished C handle (ddr_graph_build_device_finish)."""
+        g = cls.__new__(cls)
+        g._handle = handle
+        g.host_only = False
+        g.device = device
+        g.device_built = device_built
+        info = _lib.GraphInfo()
+        _lib.check(_lib.load().ddr_graph_get_info(handle, C.byref(info)))
+        g.info = GraphInfo(**{f: int(getattr(info, f)) for f, _ in _lib.GraphInfo._fields_})
+        g.n = g.info.n
+        return g
+
     def fingerprint(self) -> int:
         """Hash of the whole schedule (equal for a host and a device build of the same COO)."""
         fp = C.c_uint64()
@@ -278,6 +292,68 @@ class RiverGraph:
                 f"cut={i.n_cut}, depth={i.max_depth}, kr={i.reaches_per_thread}, generations={i.generations})")
 
 
+class PendingGraph:
+    """A device build begun on a stream (``ddr_graph_build_device_begin``): every device pass up to the
+    piece table is enqueued and nothing waits; :meth:`finish` (later, typically a training step on)
+    packs the pieces on the host, enqueues the schedule emission on the same stream and returns the
+    :class:`RiverGraph`.  Host COO arrays go up through pinned memory, so beginning never blocks."""
+
+    def __init__(self, n: int, rows, cols, *, device=None, stream=None, max_block_reaches: int = 0,
+                 target_blocks: int = 0, max_resident: int = 0, steps_hint: int = 0):
+        import torch
+
+        if isinstance(rows, torch.Tensor) and rows.is_cuda:
+            dev = rows.device
+        else:
+            dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.device = dev
+        self.stream = stream if stream is not None else torch.cuda.current_stream(dev)
+        opts = _lib.BuildOpts(0, int(max_block_reaches), int(target_blocks), int(max_resident), int(steps_hint))
+
+        def up(a):
+            if isinstance(a, torch.Tensor) and a.is_cuda:
+                return a.to(dev, torch.int32).contiguous()
+            h = torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int32))).pin_memory()
+            return h.to(dev, non_blocking=True)
+
+        with torch.cuda.device(dev), torch.cuda.stream(self.stream):
+            # (the pinned host copies are released only after the device copies: the caching host
+            # allocator records the stream)
+            self._rows, self._cols = up(rows), up(cols)
+        if self._rows.shape != self._cols.shape:
+            raise ValueError("rows and cols must have the same length")
+        h = C.c_void_p()
+        with torch.cuda.device(dev):
+            _lib.check(_lib.load().ddr_graph_build_device_begin(int(n), self._rows.numel(), self._rows.data_ptr(),
+                                                                 self._cols.data_ptr(), C.byref(opts),
+                                                                 self.stream.cuda_stream, C.byref(h)))
+        self._pending = h
+
+    def finish(self) -> RiverGraph:
+        import torch
+
+        if self._pending is None:
+            raise RuntimeError("build already finished")
+        out = C.c_void_p()
+        p, self._pending = self._pending, None
+        with torch.cuda.device(self.device):
+            _lib.check(_lib.load().ddr_graph_build_device_finish(p, C.byref(out)))
+        # the COO tensors were allocated on the build stream: their memory is reused only in its order
+        self._rows = self._cols = None
+        return RiverGraph._adopt(out, self.device, True)
+
+    def cancel(self) -> None:
+        if self._pending is not None:
+            _lib.load().ddr_graph_build_device_cancel(self._pending)
+            self._pending = None
+
+    def __del__(self):
+        try:
+            self.cancel()
+        except Exception:
+            pass
+
+
 class GraphPrefetcher:
     """Builds the routing graphs of upcoming batches on host threads, ahead of their use.
 
@@ -287,16 +363,30 @@ class GraphPrefetcher:
     keeps up to ``depth`` builds in flight on ``workers`` threads (the C build releases the GIL) and
     yields uploaded :class:`RiverGraph` objects in order; the upload (~10 ms) runs on the consumer's
     thread.  ``on_device=True`` builds on the device instead (``ddr_graph_build_device``: each builder
-    thread on its own high-priority stream; nothing per reach runs on the host).  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
+    thread on its own high-priority stream; nothing per reach runs on the host).  ``on_device="inline"``
+    (the training loop's choice): :class:`PendingGraph` builds begun ``depth`` batches ahead on the
+    consumer's stream, finished when taken -- no threads, and the build's short kernels never wait
+    behind the training step's persistent routing launches.  ``coo_iter`` yields ``(n, rows, cols)`` or ``(n, rows, cols, payload)``; the payload
     (e.g. the batch's RoutingDataclass) is returned alongside the graph.  ``upload=False`` yields the
     host-only builds (upload them with :meth:`RiverGraph.upload`).
     """
 
     def __init__(self, coo_iter, *, workers: int = 4, depth: int | None = None, device=None, upload: bool = True,
-                 on_device: bool = False, **build_kw):
+                 on_device: bool | str = False, **build_kw):
         from concurrent.futures import ThreadPoolExecutor
 
         self._it = iter(coo_iter)
+        self._inline = on_device == "inline"
+        if self._inline:
+            # device builds begun on the consumer's own stream, ``depth`` batches ahead: each next()
+            # finishes the oldest (host packing, emission enqueued) and begins the next one -- no
+            # threads, no host waits, nothing competing with the training kernels for the device
+            self._kw = dict(build_kw)
+            self._device = device
+            self._depth = max(1, int(depth if depth is not None else 2))
+            self._q = []
+            self._fill_inline()
+            return
         self._on_device = bool(on_device)
         if self._on_device:
             import threading
@@ -330,6 +420,15 @@ class GraphPrefetcher:
             return g, (rest[0] if rest else None)
         return RiverGraph(n, rows, cols, host_only=True, **self._kw), (rest[0] if rest else None)
 
+    def _fill_inline(self):
+        while len(self._q) < self._depth:
+            try:
+                item = next(self._it)
+            except StopIteration:
+                break
+            n, rows, cols, *rest = item
+            self._q.append((PendingGraph(n, rows, cols, device=self._device, **self._kw), rest[0] if rest else None))
+
     def _fill(self):
         while len(self._q) < self._depth:
             try:
@@ -342,6 +441,13 @@ class GraphPrefetcher:
         return self
 
     def __next__(self):
+        if self._inline:
+            if not self._q:
+                raise StopIteration
+            pg, payload = self._q.pop(0)
+            g = pg.finish()
+            self._fill_inline()
+            return g, payload
         if not self._q:
             self._pool.shutdown(wait=False)
             raise StopIteration
@@ -353,6 +459,11 @@ class GraphPrefetcher:
         return g, payload
 
     def close(self):
+        if self._inline:
+            for pg, _ in self._q:
+                pg.cancel()
+            self._q.clear()
+            return
         for f in self._q:
             f.cancel()
         self._q.clear()

@@ -102,6 +102,17 @@ ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int3
  * device-resident (ddr_graph_csr / ddr_graph_structure copy them to the host on request). */
 ddr_status ddr_graph_build_device(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                                   const ddr_build_opts* opts, void* stream, ddr_graph** out);
+/* The same build in two halves, for a training loop that builds batch k + d while it trains on batch
+ * k, all on its own stream: _begin enqueues every device pass up to the piece table and its copy to
+ * pinned host memory and returns at once (no host wait); _finish waits for that copy (long complete
+ * when begun a step or more ahead), packs the pieces on the host and enqueues the schedule emission
+ * on the same stream.  _finish consumes the pending build (also on error); _cancel drops one unused.
+ * rows / cols must stay valid until _finish returns. */
+typedef struct ddr_graph_pending ddr_graph_pending;
+ddr_status ddr_graph_build_device_begin(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                        const ddr_build_opts* opts, void* stream, ddr_graph_pending** out);
+ddr_status ddr_graph_build_device_finish(ddr_graph_pending* p, ddr_graph** out);
+ddr_status ddr_graph_build_device_cancel(ddr_graph_pending* p);
 /* FNV-1a hash of a graph's whole schedule (per-reach arrays, block descriptors): equal for a host and
  * a device build of the same COO and options.  Synchronous (copies the device schedule). */
 ddr_status ddr_graph_fingerprint(const ddr_graph* g, uint64_t* fp);

@@ -179,3 +179,27 @@ def test_device_collate_equals_host_collate(cuda):
     with pytest.raises(_lib.DDRError) as e:
         collate_gauges_device(5, [(np.array([1]), np.array([3]), 1)], cuda)
     assert e.value.code == _lib.DDR_ERR_NOT_LOWER
+
+
+def test_pending_builds_begun_ahead_match_host_builds(cuda):
+    """ddr_graph_build_device_begin / _finish (PendingGraph, GraphPrefetcher(on_device="inline")): builds
+    begun several batches ahead on one stream and finished in order equal the host builds; a cancelled
+    pending build releases cleanly; an invalid network raises at finish."""
+    from ddr_amd.graph import GraphPrefetcher, PendingGraph
+
+    nets = [synthetic.forest(synthetic.loguniform_sizes(20, 50, 3000, s), seed=s, single_inflow=0.25) for s in range(5)]
+    pf = GraphPrefetcher(((nt.n, nt.rows, nt.cols, i) for i, nt in enumerate(nets)), on_device="inline", depth=3,
+                         steps_hint=240)
+    seen = 0
+    for g, i in pf:
+        nt = nets[i]
+        assert g.device_built
+        assert g.fingerprint() == RiverGraph(nt.n, nt.rows, nt.cols, steps_hint=240).fingerprint()
+        g.close()
+        seen += 1
+    assert seen == len(nets)
+    PendingGraph(nets[0].n, nets[0].rows, nets[0].cols).cancel()
+    bad = PendingGraph(4, np.array([2, 3], np.int32), np.array([1, 1], np.int32))
+    with pytest.raises(_lib.DDRError) as e:
+        bad.finish()
+    assert e.value.code == _lib.DDR_ERR_NOT_DENDRITIC
