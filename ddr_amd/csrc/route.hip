@@ -595,13 +595,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
           if (off[k] >> 16) store_granule(a.bnd + (int64_t)(B.cout0 + (off[k] >> 16) - 1) * T + t, x);
-          if (t == T - 1) {
-            if (a.q_last) static_cast<R*>(a.q_last)[ref[k]] = Qn;
-            if (t > 0 && !accum) {
-              if (a.tw_last) static_cast<R*>(a.tw_last)[ref[k]] = ph[h].tw;
-              if (a.ss_last) static_cast<R*>(a.ss_last)[ref[k]] = ph[h].ss;
-            }
-          }
+          // (the last step's Q, top width and side slope: route_last_kernel, from the saved states --
+          // no rarely taken stores, and no pointers held across the tick loop for them)
           Q[k] = Qn;
           In[k] = inn;
         }
@@ -651,6 +646,52 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #endif
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
   phz.flush(a.prof, a.nblocks, bid);
+}
+
+// The forward's last-step outputs (mmc.py:441 _discharge_t, mmc.py:161-162 top_width / side_slope), from
+// the saved states: Q(T - 1) = clamp(x(T - 1)), and the geometry of step T - 1, whose physics ran on
+// Q(T - 2) -- the same operations on the same values as the routing kernel's, so the same bits.  One
+// thread per internal position.
+template <typename R, int MATH>
+__global__ void __launch_bounds__(256) route_last_kernel(RouteArgs a) {
+  load_math_tables();
+  __syncthreads();
+  const int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= a.N) return;
+  const BlockDesc B = a.s.blocks[a.s.block_of_pos[P]];
+  const int r = (int)(P - B.pos0);
+  const int64_t off = a.s.off[P];
+  const int ref = a.s.ref[P];
+  const int64_t T = a.T;
+  const R* xs = static_cast<const R*>(a.x_save) + T * B.pos0 + B.pre_dn;
+  const bool carry = a.flags & DDR_FWD_CARRY;
+  const bool accum = a.flags & DDR_FWD_ACCUMULATE;
+  const Consts<R> cs = consts_of<R>(a, false);
+  auto Q_at = [&](int64_t t) {  // Q(t): the carried state at t = 0 is not clamped
+    const R x = xs[(t + off) * B.nloc + r];
+    return (t == 0 && carry) ? x : rmax_nan(x, cs.qlb);
+  };
+  if (a.q_last) static_cast<R*>(a.q_last)[ref] = Q_at(T - 1);
+  if (T > 1 && !accum && (a.tw_last || a.ss_last)) {
+    const ReachStatic<R> st = load_static<R>(a, ref);
+    const R Qv = Q_at(T - 2);
+    PhysOut<R> ph;
+    constexpr bool kFast = MATH == 1 && std::is_same<R, float>::value;
+    constexpr bool kFaith = MATH == 2 && std::is_same<R, float>::value;
+    if constexpr (kFast) {
+      ph = coefficients_fast(st, Qv, cs);
+    } else if constexpr (kFaith) {
+      ph = coefficients_faithful(st, Qv, cs);
+    } else {
+      ReachStatic<R> sa[1] = {st};
+      R qa[1] = {Qv};
+      PhysOut<R> pa[1];
+      coefficients_np<R, 1>(sa, qa, cs, pa);
+      ph = pa[0];
+    }
+    if (a.tw_last) static_cast<R*>(a.tw_last)[ref] = ph.tw;
+    if (a.ss_last) static_cast<R*>(a.ss_last)[ref] = ph.ss;
+  }
 }
 
 template <typename R>
@@ -1370,6 +1411,16 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (a.q_last || a.tw_last || a.ss_last) {
+      auto last = route_last_kernel<R, 0>;
+      if constexpr (std::is_same<R, float>::value) {
+        if (a.flags & DDR_FWD_FAST_MATH) last = route_last_kernel<R, 1>;
+        else if (a.flags & DDR_FWD_FAITHFUL_MATH) last = route_last_kernel<R, 2>;
+      }
+      hipLaunchKernelGGL(last, dim3((unsigned)((g->n + 255) / 256)), dim3(256), kMathTabBytes, stream, a);
+    }
   }
   return hipGetLastError();
 }

@@ -194,5 +194,7 @@ def test_geometry_statistics_long_window(cuda, D):
     for k, v in got.items():
         assert np.array_equal(np.isnan(v), np.isnan(orc[k])), k
         ok = ~np.isnan(orc[k])
-        tol = 1e-6 if k.endswith("_mean") else 0.0
+        # means: the kernel sums in fp64, numpy's nanmean pairwise in fp32 -- a few ulp apart over
+        # hundreds of days (as test_c4_full_size_sampled_basins); min / max / median exact
+        tol = 5e-6 if k.endswith("_mean") else 0.0
         assert maxrel(v[ok], orc[k][ok]) <= tol, (D, k)
