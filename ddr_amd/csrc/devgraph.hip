@@ -572,8 +572,8 @@ struct DevBuild {
   explicit DevBuild(hipStream_t st) : s(st), scr(st) {}
   ~DevBuild() {
     if (tab_ev) (void)hipEventDestroy(tab_ev);
-    if (pin) (void)hipHostFree(pin);
-    if (ptab) (void)hipHostFree(ptab);
+    pinned_put(pin, s);  // its copies were waited for (read_table), or are queued on s
+    pinned_put(ptab, s);
   }
   const ddr_build_opts* options() const { return has_opts ? &opts : nullptr; }
 
@@ -697,9 +697,10 @@ struct DevBuild {
     tab = scr.get<int32_t>(8 * n);
     DDR_SCR(resid); DDR_SCR(stem); DDR_SCR(is_root); DDR_SCR(pflag); DDR_SCR(prank); DDR_SCR(q); DDR_SCR(dloc);
     DDR_SCR(piece); DDR_SCR(tab);
-    DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&pin), sizeof(Pinned), hipHostMallocDefault));
+    pin = static_cast<Pinned*>(pinned_get(sizeof(Pinned)));
     guess = std::min<int64_t>(n, 16384);
-    DDR_HIP(hipHostMalloc(reinterpret_cast<void**>(&ptab), sizeof(int32_t) * 8 * (size_t)guess, hipHostMallocDefault));
+    ptab = static_cast<int32_t*>(pinned_get(sizeof(int32_t) * 8 * (size_t)guess));
+    if (!pin || !ptab) return fail(DDR_ERR_HIP, "device graph: pinned host memory");
     DDR_HIP(hipEventCreateWithFlags(&tab_ev, hipEventDisableTiming));
     D = n - 1;
     return pass();
@@ -868,7 +869,8 @@ struct DevBuild {
     }
     // host sources of the asynchronous uploads live as long as the graph (pinned: truly asynchronous)
     const size_t nstage = sizeof(BlockDesc) * (size_t)nb + sizeof(int32_t) * ((size_t)pt.count() + (size_t)nb);
-    DDR_HIP(hipHostMalloc(&g->staging, std::max<size_t>(nstage, 16), hipHostMallocDefault));
+    g->staging = pinned_get(std::max<size_t>(nstage, 16));
+    if (!g->staging) return fail(DDR_ERR_HIP, "device graph: pinned host memory");
     BlockDesc* hblk = static_cast<BlockDesc*>(g->staging);
     std::copy(g->blocks.begin(), g->blocks.end(), hblk);
     int32_t* hbop = reinterpret_cast<int32_t*>(hblk + nb);

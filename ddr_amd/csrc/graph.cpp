@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <memory>
+#include <mutex>
 #include <numeric>
 
 #include "internal.h"
@@ -652,13 +653,58 @@ void destroy_graph(Graph* g, hipStream_t stream) {
   for (void* p : g->allocations) (void)hipFree(p);
   if (g->ready) (void)hipStreamWaitEvent(stream, g->ready, 0);  // the build's last work precedes the free
   for (void* p : g->async_allocations) (void)hipFreeAsync(p, stream);
-  if (g->staging) {
-    // the build's uploads read it: long complete by the time a graph is released
-    if (g->ready) (void)hipEventSynchronize(g->ready);
-    (void)hipHostFree(g->staging);
-  }
+  // the build's uploads read the staging block: reusable once `stream` has passed the build
+  if (g->staging) pinned_put(g->staging, stream);
   if (g->ready) (void)hipEventDestroy(g->ready);
   delete g;
+}
+
+namespace {
+struct PinnedBlock {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;  // recorded at return; the block is free once it has fired
+  bool out = false;         // handed out
+};
+std::mutex g_pinned_mu;
+std::vector<PinnedBlock> g_pinned;  // never freed: hipHostFree would synchronise with the device
+}  // namespace
+
+void* pinned_get(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 64);
+  size_t cls = 64;
+  while (cls < bytes) cls <<= 1;  // power-of-two classes: blocks of a stream of batches get reused
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  for (PinnedBlock& b : g_pinned) {
+    if (b.out || b.bytes != cls) continue;
+    if (b.ev && hipEventQuery(b.ev) != hipSuccess) continue;  // still read by queued copies
+    b.out = true;
+    return b.p;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) return nullptr;
+  PinnedBlock b;
+  b.p = p;
+  b.bytes = cls;
+  b.out = true;
+  g_pinned.push_back(b);
+  return p;
+}
+
+void pinned_put(void* p, hipStream_t s) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pinned_mu);
+  for (PinnedBlock& b : g_pinned) {
+    if (b.p != p) continue;
+    if (!b.ev) (void)hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
+    if (b.ev && hipEventRecord(b.ev, s) != hipSuccess) {
+      (void)hipEventDestroy(b.ev);  // not recordable: wait here rather than hand out a block in use
+      b.ev = nullptr;
+      (void)hipStreamSynchronize(s);
+    }
+    b.out = false;
+    return;
+  }
 }
 
 }  // namespace ddr

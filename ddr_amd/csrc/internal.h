@@ -206,6 +206,14 @@ const char* last_error_cstr();
     if (_e != hipSuccess) return ::ddr::hip_fail(_e, #call); \
   } while (0)
 
+// Pinned host blocks reused across builds (graph.cpp).  hipHostFree waits for every queued device
+// operation, so releasing a batch's staging memory that way stalled a training loop's host behind the
+// previous step's routing launches (the C3 stream's 28-74 ms graph waits).  pinned_put(p, s) returns a
+// block once the work queued on `s` so far is done (an event recorded on `s`); pinned_get reuses a
+// returned block of at least `bytes` whose event has fired, or allocates.  Blocks live until exit.
+void* pinned_get(size_t bytes);
+void pinned_put(void* p, hipStream_t s);
+
 // graph.cpp
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                        const ddr_build_opts* opts, Graph** out);
