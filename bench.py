@@ -548,11 +548,21 @@ def time_training_stream(args, dev):
     pf.close()
     rs = sum(b["reaches"] for b in per) * (T - 1)
     waits = [b["graph_wait_ms"] for b in per]
+    gpu = float(np.mean([b["step_gpu_ms"] for b in per]))
     return {"steps": K, "ms_per_step": timed / K * 1e3, "value": rs / timed, "unit": "reach-timesteps/s",
             "graph_builder": args.stream_builder, "graph_workers": args.stream_workers,
-            "graph_wait_ms_mean": float(np.mean(waits)) if waits else None, "batches": per,
+            "graph_wait_ms_mean": float(np.mean(waits)) if waits else None,
+            "step_gpu_ms_mean": gpu,
+            # wall time per step not inside a training step's own GPU span: the next batches' device
+            # builds (queued between steps on the training stream) and any device idle time
+            "between_steps_ms": timed / K * 1e3 - gpu,
+            "ns_per_reach_step_gpu": float(np.mean([b["step_gpu_ms"] * 1e6 / (b["reaches"] * (T - 1)) for b in per])),
+            "batches": per,
             "note": (f"new adjacency + graph build per step ({BUILDERS[args.stream_builder]}"
-                     f", overlapped with training), {M} distinct batches cycled")}
+                     f", overlapped with training), {M} distinct batches cycled; graph_wait_ms is host time in "
+                     "g.close() + next(prefetcher), i.e. it includes the host waiting for queued device work "
+                     "(back-pressure), which costs nothing while the device is busy: between_steps_ms is the "
+                     "device-side cost")}
 
 
 def time_dropin(args, net, at, u, qprime, W, dev):

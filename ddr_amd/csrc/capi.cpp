@@ -579,8 +579,8 @@ ddr_status ddr_hotstart_f32(const ddr_graph* gh, const float* q, double discharg
     // one forward step in accumulation mode (every step a hot start, no coefficient physics): its
     // workspace is stream-ordered scratch; the per-reach statics are never read for their values
     const size_t xs = sizeof(float) * 2 * (size_t)(g->n + g->sum_dn);
-    void* ws = nullptr;
-    DDR_HIP(hipMallocAsync(&ws, xs + sizeof(double) * (size_t)std::max<int64_t>(g->n_cut, 1) + kStatusBytes, s));
+    void* ws = device_get(xs + sizeof(double) * (size_t)std::max<int64_t>(g->n_cut, 1) + kStatusBytes, s);
+    if (!ws) return fail(DDR_ERR_HIP, "hot start: out of device memory");
     ddr_mc_consts c;
     c.dt = 3600.0;
     c.discharge_lb = discharge_lb;
@@ -597,7 +597,7 @@ ddr_status ddr_hotstart_f32(const ddr_graph* gh, const float* q, double discharg
     ddr_status st = forward_impl<float>(gh, &c, &r, q, 1, nullptr, out, reinterpret_cast<float*>(base),
                                         reinterpret_cast<double*>(base + xs), base + xs + sizeof(double) * std::max<int64_t>(g->n_cut, 1),
                                         nullptr, nullptr, nullptr, DDR_FWD_ACCUMULATE, stream);
-    (void)hipFreeAsync(ws, s);
+    device_put(ws, s);
     return st;
   })
 }

@@ -16,7 +16,7 @@
 //   upstream lists and confluence lists in position order).
 //
 // The host reads the device twice per split pass (a count, then the piece table); everything per
-// reach stays on the device.  Temporaries are stream-ordered (hipMallocAsync) on the build stream.
+// reach stays on the device.  Temporaries are pooled device blocks (device_get) ordered on the build stream.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -444,7 +444,7 @@ __global__ void k_outflow_fill(int64_t G, const int32_t* gage_c, const int32_t* 
   for (int32_t k = k0; k < k1; ++k) out_idx[o + (k - k0)] = col[k];
 }
 
-// Stream-ordered temporaries of one build, released (stream-ordered) when the build returns.
+// Temporaries of one build (pooled device blocks), returned stream-ordered when the build returns.
 struct Scratch {
   hipStream_t s;
   std::vector<void*> ptrs;
@@ -452,23 +452,22 @@ struct Scratch {
   explicit Scratch(hipStream_t st) : s(st) {}
   template <typename T>
   T* get(int64_t n) {
-    void* p = nullptr;
-    const hipError_t e = hipMallocAsync(&p, (size_t)std::max<int64_t>(n, 1) * sizeof(T), s);
-    if (e != hipSuccess) {
-      err = e;
+    void* p = device_get((size_t)std::max<int64_t>(n, 1) * sizeof(T), s);
+    if (!p) {
+      err = hipErrorOutOfMemory;
       return nullptr;
     }
     ptrs.push_back(p);
     return static_cast<T*>(p);
   }
   ~Scratch() {
-    for (void* p : ptrs) (void)hipFreeAsync(p, s);
+    for (void* p : ptrs) device_put(p, s);
   }
 };
 
 #define DDR_SCR(ptr)                                                        \
   do {                                                                      \
-    if (!(ptr)) return ::ddr::hip_fail(scr.err, "device graph: hipMallocAsync"); \
+    if (!(ptr)) return ::ddr::hip_fail(scr.err, "device graph: scratch allocation"); \
   } while (0)
 
 template <typename T>
@@ -511,17 +510,6 @@ ddr_status jump(Scratch& scr, int64_t n, const int32_t* down, const uint8_t* sto
 
 // The default memory pool returns freed memory to the driver at every synchronisation unless told to
 // keep it: a build per training batch would then pay fresh allocations each time.
-void keep_pool_warm() {
-  static bool done = false;
-  if (done) return;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess) return;
-  uint64_t thr = ~0ull;
-  (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-  done = true;
-}
 
 int log2_rounds(int64_t len) {
   int r = 1;
@@ -590,7 +578,6 @@ struct DevBuild {
     g->n = n;
     g->nnz = e;
     double tp = now_ms();
-    keep_pool_warm();
     // ---- validation, down[], CSR --------------------------------------------------------------
     down = scr.get<int32_t>(n);
     deg = scr.get<int32_t>(n + 1);
@@ -826,10 +813,10 @@ struct DevBuild {
                           + 11 * n + e               // ref off upb upc dloc cut xoff pos_of_ref block_of_pos rs_loc rs_ref, uplist
                           + 4 * ncut + nx_total;     // v_edge v_off v_dloc cout_loc, xlist
     const size_t bytes = sizeof(int32_t) * (size_t)words + sizeof(BlockDesc) * (size_t)nb + 64;
-    // stream-ordered (the default pool, kept warm): freeing a batch's graph (ddr_graph_destroy_async on
-    // the training stream) then needs no device-wide synchronisation, unlike hipFree
-    void* slab = nullptr;
-    DDR_HIP(hipMallocAsync(&slab, bytes, s));
+    // a pooled block: releasing a batch's graph (ddr_graph_destroy_async on the training stream) is
+    // stream-ordered and never waits on the host (neither hipFree nor hipFreeAsync is called)
+    void* slab = device_get(bytes, s);
+    if (!slab) return fail(DDR_ERR_HIP, "device graph: out of device memory");
     g->async_allocations.push_back(slab);
     int32_t* w = static_cast<int32_t*>(slab);
     auto carve = [&](int64_t k) {

@@ -652,7 +652,7 @@ void destroy_graph(Graph* g, hipStream_t stream) {
   if (!g) return;
   for (void* p : g->allocations) (void)hipFree(p);
   if (g->ready) (void)hipStreamWaitEvent(stream, g->ready, 0);  // the build's last work precedes the free
-  for (void* p : g->async_allocations) (void)hipFreeAsync(p, stream);
+  for (void* p : g->async_allocations) device_put(p, stream);
   // the build's uploads read the staging block: reusable once `stream` has passed the build
   if (g->staging) pinned_put(g->staging, stream);
   if (g->ready) (void)hipEventDestroy(g->ready);
@@ -660,41 +660,28 @@ void destroy_graph(Graph* g, hipStream_t stream) {
 }
 
 namespace {
-struct PinnedBlock {
+// One pool for pinned host blocks (device = -1) and device blocks (device id).  Blocks are never
+// freed (hipHostFree and hipFree synchronise with the device); sizes are power-of-two classes.
+struct PoolBlock {
   void* p = nullptr;
   size_t bytes = 0;
-  hipEvent_t ev = nullptr;  // recorded at return; the block is free once it has fired
+  int device = -1;
+  hipEvent_t ev = nullptr;  // recorded at return
   bool out = false;         // handed out
 };
-std::mutex g_pinned_mu;
-std::vector<PinnedBlock> g_pinned;  // never freed: hipHostFree would synchronise with the device
-}  // namespace
+std::mutex g_pool_mu;
+std::vector<PoolBlock> g_pool;
 
-void* pinned_get(size_t bytes) {
-  bytes = std::max<size_t>(bytes, 64);
-  size_t cls = 64;
-  while (cls < bytes) cls <<= 1;  // power-of-two classes: blocks of a stream of batches get reused
-  std::lock_guard<std::mutex> lk(g_pinned_mu);
-  for (PinnedBlock& b : g_pinned) {
-    if (b.out || b.bytes != cls) continue;
-    if (b.ev && hipEventQuery(b.ev) != hipSuccess) continue;  // still read by queued copies
-    b.out = true;
-    return b.p;
-  }
-  void* p = nullptr;
-  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) return nullptr;
-  PinnedBlock b;
-  b.p = p;
-  b.bytes = cls;
-  b.out = true;
-  g_pinned.push_back(b);
-  return p;
+size_t size_class(size_t bytes) {
+  size_t cls = 256;
+  while (cls < bytes) cls <<= 1;
+  return cls;
 }
 
-void pinned_put(void* p, hipStream_t s) {
+void pool_put(void* p, hipStream_t s) {
   if (!p) return;
-  std::lock_guard<std::mutex> lk(g_pinned_mu);
-  for (PinnedBlock& b : g_pinned) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (PoolBlock& b : g_pool) {
     if (b.p != p) continue;
     if (!b.ev) (void)hipEventCreateWithFlags(&b.ev, hipEventDisableTiming);
     if (b.ev && hipEventRecord(b.ev, s) != hipSuccess) {
@@ -706,5 +693,50 @@ void pinned_put(void* p, hipStream_t s) {
     return;
   }
 }
+}  // namespace
+
+void* pinned_get(size_t bytes) {
+  const size_t cls = size_class(bytes);
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (PoolBlock& b : g_pool) {
+    if (b.out || b.device != -1 || b.bytes != cls) continue;
+    if (b.ev && hipEventQuery(b.ev) != hipSuccess) continue;  // still read by queued copies
+    b.out = true;
+    return b.p;
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) return nullptr;
+  PoolBlock b;
+  b.p = p;
+  b.bytes = cls;
+  b.out = true;
+  g_pool.push_back(b);
+  return p;
+}
+void pinned_put(void* p, hipStream_t s) { pool_put(p, s); }
+
+void* device_get(size_t bytes, hipStream_t s) {
+  const size_t cls = size_class(bytes);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (PoolBlock& b : g_pool) {
+    if (b.out || b.device != dev || b.bytes != cls) continue;
+    // the last user's work (queued on its stream) precedes this one's, without a host wait
+    if (b.ev && hipStreamWaitEvent(s, b.ev, 0) != hipSuccess) continue;
+    b.out = true;
+    return b.p;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, cls) != hipSuccess) return nullptr;
+  PoolBlock b;
+  b.p = p;
+  b.bytes = cls;
+  b.device = dev;
+  b.out = true;
+  g_pool.push_back(b);
+  return p;
+}
+void device_put(void* p, hipStream_t s) { pool_put(p, s); }
 
 }  // namespace ddr

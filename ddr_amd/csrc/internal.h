@@ -154,7 +154,7 @@ struct Graph {
   hipEvent_t ready = nullptr;  // device builds: recorded on the build stream once the schedule is complete
   void* staging = nullptr;     // pinned host sources of the device build's last uploads
   std::vector<void*> allocations;        // hipMalloc (host builds)
-  std::vector<void*> async_allocations;  // hipMallocAsync (device builds): freed stream-ordered
+  std::vector<void*> async_allocations;  // device_get blocks (device builds): returned stream-ordered
 };
 
 // ---- piece-level packing, shared by the host builder (graph.cpp) and the device builder ---------
@@ -213,6 +213,13 @@ const char* last_error_cstr();
 // returned block of at least `bytes` whose event has fired, or allocates.  Blocks live until exit.
 void* pinned_get(size_t bytes);
 void pinned_put(void* p, hipStream_t s);
+// Device blocks reused the same way (graph.cpp), for the per-batch build scratch and graph arrays:
+// hipFreeAsync blocked the host 5-44 ms per call in the training stream (profiles/r03), leaving the
+// device idle while the host caught up.  device_get(bytes, s) hands out a free block of the current
+// device and makes `s` wait (hipStreamWaitEvent, no host wait) for the work queued when it was
+// returned; device_put(p, s) returns it after the work queued on `s` so far.  hipMalloc only grows.
+void* device_get(size_t bytes, hipStream_t s);
+void device_put(void* p, hipStream_t s);
 
 // graph.cpp
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
