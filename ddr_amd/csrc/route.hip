@@ -583,8 +583,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if (hk && t >= 0 && t < T) {
           const R xr = R(x);
           const R Qn = raw ? xr : rmax_nan(xr, cs.qlb);
-          xrow[r] = xr;  // the routing state for the adjoint
-          if (emit) {
+#ifndef DDR_EXP_NO_FWD_STORES
+#define DDR_EXP_NO_FWD_STORES 0  // timing experiment only: no x_save / runoff stores (wrong results)
+#endif
+          if (!DDR_EXP_NO_FWD_STORES) xrow[r] = xr;  // the routing state for the adjoint
+          if (emit && !DDR_EXP_NO_FWD_STORES) {
             // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
             ob0[k] = ob1[k];
             ob1[k] = ob2[k];

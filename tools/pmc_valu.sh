@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 [ -n "$V" ] && export DDR_LIB=$R/ddr_amd/lib/libddr_mc_$V.so
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --no-cpu-baseline"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --dropin-steps 0 ${BENCH_ARGS:-}"
 run() {
   local n=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" -d $OUT/$n -o run -- python3 $R/bench.py $ARGS > $OUT/$n.log 2>&1
