@@ -40,6 +40,7 @@ DDR_FWD_FAST_MATH = 16
 DDR_FWD_FAITHFUL_MATH = 32
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
+DDR_DEBUG_NO_STEADY = 2
 
 
 class BuildOpts(C.Structure):

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <mutex>
@@ -43,7 +44,10 @@ struct KernelTiming {
   bool recorded[2] = {false, false};
 } g_timing;
 unsigned long long* g_prof[2] = {nullptr, nullptr};
-int32_t g_debug = 0;  // ddr_set_debug_flags
+int32_t g_debug = [] {  // ddr_set_debug_flags (DDR_NO_STEADY=1: the general tick path only, for A/B)
+  const char* e = std::getenv("DDR_NO_STEADY");
+  return (e && e[0] == '1') ? kFlagNoSteady : 0;
+}();
 
 // Hand-off failures surface without a host sync on the hot path: after every routing launch the
 // status block's first words are copied (async, same stream) into a pinned slot with an event
@@ -681,7 +685,7 @@ ddr_status ddr_status_check(int32_t wait) {
 }
 
 ddr_status ddr_set_debug_flags(int32_t flags) {
-  g_debug = (flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0;
+  g_debug = ((flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0) | ((flags & DDR_DEBUG_NO_STEADY) ? kFlagNoSteady : 0);
   return DDR_OK;
 }
 

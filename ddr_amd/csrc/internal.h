@@ -264,5 +264,6 @@ constexpr int kStatusTicketFwd = 2;
 constexpr int kStatusTicketBwd = 3;
 // RouteArgs.flags bits beyond the public DDR_FWD_* flags
 constexpr int32_t kFlagForceTimeout = 1 << 16;  // debug: every inter-workgroup wait times out
+constexpr int32_t kFlagNoSteady = 1 << 17;      // debug / A/B: every tick through the general path
 
 }  // namespace ddr

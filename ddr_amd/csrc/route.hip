@@ -49,6 +49,9 @@ namespace ddr {
 #ifndef DDR_SKIP_IDLE_BWD
 #define DDR_SKIP_IDLE_BWD 0
 #endif
+#ifndef DDR_BWD_STEADY
+#define DDR_BWD_STEADY 1
+#endif
 #ifndef DDR_BWD_EARLY_MAX_KR
 #define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
 #endif
@@ -446,7 +449,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // carried Q0 at t = 0, for the step each reach runs at tick `tau`
   const R* qsb = static_cast<const R*>(a.qs) + xs_base;
   const bool qs_rows = a.qs_rows > 0;
-  auto prefetch = [&](int tau, R(&dst)[KR], int tq0) {
+  // kSt (steady ticks, below): no reach is at its carried t = 0 step
+  auto prefetch = [&](int tau, R(&dst)[KR], int tq0, auto sc) {
+    constexpr bool kSt = decltype(sc)::value;
     const R* row = qsb + (int64_t)(tau < TTf ? tau : TTf - 1) * B.nloc;
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
@@ -454,11 +459,15 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int r = tq0 + k * BS;
       const int rs = r < B.nloc ? r : 0;
       const R v = qs_rows ? *qs_at<R>(a, B, xs_base, tau, off_of(k), rs) : row[rs];
-      dst[k] = (carry && tau == off_of(k)) ? q0p[ref[k]] : v;
+      dst[k] = (!kSt && carry && tau == off_of(k)) ? q0p[ref[k]] : v;
     }
   };
 
-  auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR]) {
+  // sc: std::integral_constant<bool, kSt>.  Steady ticks (tau in [dmax + 1, T - 1]) are those at which
+  // every reach of the block runs a step t in [1, T - 1]: no activity tests, no idle-slice ballot, no
+  // hot start or carried-state case -- the same operations on the same values as the general tick
+  auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR], auto sc) {
+    constexpr bool kSt = decltype(sc)::value;
 #if DDR_FWD_TOPWAIT
     // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
@@ -496,7 +505,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     phz.mark(1);  // import
-    prefetch(tau + 1, qnext, tq);
+    prefetch(tau + 1, qnext, tq, sc);
     R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
     // ---- compute, NP slices at a time: their physics in lockstep (NP independent dependency
@@ -505,7 +514,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k0 = 0; k0 < KR; k0 += NP) {
       if (wbase + k0 * BS >= B.nloc) continue;
-      if (DDR_SKIP_IDLE) {
+      if (!kSt && DDR_SKIP_IDLE) {
         // no lane of the wave runs a step this tick (before its first / after its last step: the
         // first and last dmax ticks of a block, most ticks of a short window): skip the slice
         bool act = false;
@@ -553,7 +562,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const double x0v = sx[up_0(up[k])];
         const double x1v = sx[up_1(up[k], xl)];
         // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
-        const bool raw = (t == 0 && carry);
+        const bool raw = !kSt && (t == 0 && carry);
         auto qf = [&](double x) -> R {
           const R xr = R(x);
           return raw ? xr : rmax(xr, cs.qlb);
@@ -562,9 +571,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         double acc = (double)b;                                         // utils.py:587-600 (fp64)
         acc = acc + dc1 * x0v;                                          // (+ 0 for a missing upstream)
         acc = acc + dc1 * x1v;
-        double hot = (double)qv;                                        // mmc.py:25-66 (hot start)
-        hot = hot + x0v;
-        hot = hot + x1v;
+        double hot = 0.0;
+        if constexpr (!kSt) {
+          hot = (double)qv;                                             // mmc.py:25-66 (hot start)
+          hot = hot + x0v;
+          hot = hot + x1v;
+        }
         R inn = R(0);                                                   // I(t+1) = N @ Q_t, ascending columns
         inn = inn + (nup > 0 ? qf(x0v) : R(0));
         inn = inn + (nup > 1 ? qf(x1v) : R(0));
@@ -574,13 +586,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           for (int j = 2; j < c; ++j) {
             const double xj = sx[lst[j]];
             acc = acc + dc1 * xj;
-            hot = hot + xj;
+            if constexpr (!kSt) hot = hot + xj;
             inn = inn + qf(xj);
           }
         }
-        const double x = (t == 0 && carry) ? (double)qcur[k] : ((t == 0 || accum) ? hot : acc);
+        const double x = kSt ? acc : ((t == 0 && carry) ? (double)qcur[k] : ((t == 0 || accum) ? hot : acc));
         xk[k] = x;
-        if (hk && t >= 0 && t < T) {
+        if (hk && (kSt || (t >= 0 && t < T))) {
           const R xr = R(x);
           const R Qn = raw ? xr : rmax_nan(xr, cs.qlb);
 #ifndef DDR_EXP_NO_FWD_STORES
@@ -597,7 +609,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
-          if (off[k] >> 16) store_granule(a.bnd + (int64_t)(B.cout0 + (off[k] >> 16) - 1) * T + t, x);
+          if (B.ncout > 0 && (off[k] >> 16)) store_granule(a.bnd + (int64_t)(B.cout0 + (off[k] >> 16) - 1) * T + t, x);
           // (the last step's Q, top width and side slope: route_last_kernel, from the saved states --
           // no rarely taken stores, and no pointers held across the tick loop for them)
           Q[k] = Qn;
@@ -615,7 +627,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (wbase + k * BS >= B.nloc) continue;
       const int t = tau - off_of(k);
       const int r = tq + k * BS;
-      if (r < B.nloc && t >= 0 && t < T) sx[r] = xk[k];
+      if (r < B.nloc && (kSt || (t >= 0 && t < T))) sx[r] = xk[k];
     }
     if (vown) {
       const int t = tau - v_off;
@@ -627,22 +639,43 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   const int TT = (int)T + B.dmax;
-  prefetch(0, qa, tid);
+  using Gen = std::integral_constant<bool, false>;
+  using Steady = std::integral_constant<bool, true>;
+  prefetch(0, qa, tid, Gen{});
 #if DDR_FWD_UNROLL2
   // two ticks per iteration, the prefetch registers swapping roles: copying the prefetched q'
-  // (qa = qb) at the loop latch would wait for the loads just issued, and for every store of the tick
+  // (qa = qb) at the loop latch would wait for the loads just issued, and for every store of the tick.
+  // Steady ticks [s0, s1) (even bounds, so the roles keep alternating) between the ramps.
+#ifndef DDR_FWD_STEADY
+#define DDR_FWD_STEADY 1
+#endif
+  int s0 = B.dmax + 1, s1 = (int)T & ~1;
+  s0 += s0 & 1;
+  if (!DDR_FWD_STEADY || (a.flags & kFlagNoSteady) || accum || s1 <= s0) s0 = s1 = 0;
 #pragma unroll 1
-  for (int tau = 0; tau < TT; tau += 2) {
+  for (int tau = 0; tau < s0; tau += 2) {
     if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
-    tick(tau, qa, qb);
-    if (tau + 1 < TT) tick(tau + 1, qb, qa);
+    tick(tau, qa, qb, Gen{});
+    tick(tau + 1, qb, qa, Gen{});
+  }
+#pragma unroll 1
+  for (int tau = s0; tau < s1; tau += 2) {
+    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    tick(tau, qa, qb, Steady{});
+    tick(tau + 1, qb, qa, Steady{});
+  }
+#pragma unroll 1
+  for (int tau = s1; tau < TT; tau += 2) {
+    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    tick(tau, qa, qb, Gen{});
+    if (tau + 1 < TT) tick(tau + 1, qb, qa, Gen{});
   }
 #else
   // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
 #pragma unroll 1
   for (int tau = 0; tau < TT; ++tau) {
     if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
-    tick(tau, qa, qb);
+    tick(tau, qa, qb, Gen{});
 #pragma unroll
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
@@ -890,7 +923,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 
   // xbc / vxc: loaded last tick, published now; xbn / vxn: loaded now for the next tick (the same
   // registers without early loads)
-  auto tick = [&](int tb, R(&xbc)[KR], R(&xbn)[KR], double& vxc, double& vxn) {
+  // sc: std::integral_constant<bool, kSt>.  Steady ticks (forward tick tau in [dmax + 2, T - 1]) are
+  // those at which every reach runs a step t in [2, T - 1]: no activity tests, no t = 1 carried-state
+  // case, no step-0 sweep, the next step's gradient group always in range
+  auto tick = [&](int tb, R(&xbc)[KR], R(&xbn)[KR], double& vxc, double& vxn, auto sc) {
+    constexpr bool kSt = decltype(sc)::value;
     const int tau = TT - 1 - tb;  // forward tick
     // Every global load of the previous tick (states, virtual inflows, gradient groups) lands
     // here, a whole tick after its issue.  An explicit wait the compiler can see: without it, its
@@ -977,10 +1014,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const bool hk = r < B.nloc;
       const int rs = hk ? r : 0;
       const int t = tau - off_of(k);
-      const bool active = hk && t >= 1 && t < T;
+      const bool active = hk && (kSt || (t >= 1 && t < T));
       // upstream x_j(t - 1): I(t) = sum_j Q_j(t - 1) (mmc.py:535, ascending columns; the carried
       // state at t - 1 = 0 is not clamped) and Sx(t - 1) for the next tick
-      const bool c0 = (t == 1 && carry);
+      const bool c0 = !kSt && (t == 1 && carry);
       const int nup = up_n(up[k]);
       const R x0 = sx[up_0(up[k])];
       const R x1 = sx[up_1(up[k], xl)];
@@ -1032,7 +1069,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         // flush the fp32 partial sums into the fp64 accumulators every kGradFlush *steps* (aligned to
         // t, not to ticks, so the summation grouping -- and the result -- is independent of the
         // partition); one owner per address, so the atomics are deterministic
-        if ((t % kGradFlush) == 1 || t == 1) {
+        if ((t % kGradFlush) == 1 || (!kSt && t == 1)) {
           double* g3p = gacc + (int64_t)ref[k] * 3;
           atomicAdd(g3p + 0, (double)pn[k]);
           atomicAdd(g3p + 1, (double)pq[k]);
@@ -1044,7 +1081,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         lam[k] = ((gb * c3) + gQ) + Bd[k];
         // dL/dqc = gb c4 (b = ... + c4 qc), through qc = clamp(q' * flow_scale) (mmc.py:421-424)
         if constexpr (GS) gqs[xs_base + (int64_t)tau * B.nloc + r] = (qsv[k] >= cs.qlb) ? gb * c4 : R(0);
-      } else if (GS && hk && t == 0) {
+      } else if (!kSt && GS && hk && t == 0) {
         if (carry) {
           // Q0 = q0 feeds step 1 unclamped; runoff[:, 0] = clamp(q0) per reach, or the gauge sum's clamp
           // (already folded into gk through gmask0)
@@ -1066,7 +1103,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
-      if (hk && has_grad(k) && tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)) {
+      if (hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
         const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3));
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
@@ -1124,18 +1161,49 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
   phz.start();
+  using Gen = std::integral_constant<bool, false>;
+  using Steady = std::integral_constant<bool, true>;
+  // steady backward ticks [b0, b1): forward ticks tau = TT - 1 - tb in [dmax + 2, T - 1]
+  int b0 = B.dmax, b1 = (int)T - 2;
+  if (kEarly) {  // even bounds: the register roles keep alternating
+    b0 += b0 & 1;
+    b1 &= ~1;
+  }
+  if (!DDR_BWD_STEADY || (a.flags & kFlagNoSteady) || b1 <= b0) b0 = b1 = 0;
   if constexpr (kEarly) {
 #pragma unroll 1
-    for (int tb = 0; tb < TT; tb += 2) {
+    for (int tb = 0; tb < b0; tb += 2) {
       if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
-      tick(tb, xb, xb2, vx, vx2);
-      if (tb + 1 < TT) tick(tb + 1, xb2, xb, vx2, vx);
+      tick(tb, xb, xb2, vx, vx2, Gen{});
+      tick(tb + 1, xb2, xb, vx2, vx, Gen{});
+    }
+#pragma unroll 1
+    for (int tb = b0; tb < b1; tb += 2) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb2, vx, vx2, Steady{});
+      tick(tb + 1, xb2, xb, vx2, vx, Steady{});
+    }
+#pragma unroll 1
+    for (int tb = b1; tb < TT; tb += 2) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb2, vx, vx2, Gen{});
+      if (tb + 1 < TT) tick(tb + 1, xb2, xb, vx2, vx, Gen{});
     }
   } else {
 #pragma unroll 1
-    for (int tb = 0; tb < TT; ++tb) {
+    for (int tb = 0; tb < b0; ++tb) {
       if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
-      tick(tb, xb, xb, vx, vx);
+      tick(tb, xb, xb, vx, vx, Gen{});
+    }
+#pragma unroll 1
+    for (int tb = b0; tb < b1; ++tb) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb, vx, vx, Steady{});
+    }
+#pragma unroll 1
+    for (int tb = b1; tb < TT; ++tb) {
+      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      tick(tb, xb, xb, vx, vx, Gen{});
     }
   }
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);

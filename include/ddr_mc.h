@@ -330,8 +330,10 @@ ddr_status ddr_graph_status(const void* status, void* stream);
  * counterpart (the reference solver raises ValueError on failure, routing/utils.py:598-600). */
 ddr_status ddr_status_check(int32_t wait);
 /* Debug knobs.  DDR_DEBUG_FORCE_TIMEOUT: every inter-workgroup wait of the following launches
- * times out (tests the failure path). */
-enum { DDR_DEBUG_FORCE_TIMEOUT = 1 };
+ * times out (tests the failure path).  DDR_DEBUG_NO_STEADY: the routing kernels run every tick
+ * through their general path instead of the specialised steady-tick path (bitwise A/B; also set by
+ * the environment variable DDR_NO_STEADY=1). */
+enum { DDR_DEBUG_FORCE_TIMEOUT = 1, DDR_DEBUG_NO_STEADY = 2 };
 ddr_status ddr_set_debug_flags(int32_t flags);
 
 /* General sparse triangular solve A x = b (lower) or A^T x = b (transpose = 1), CSR A with a
