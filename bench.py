@@ -188,6 +188,65 @@ def cpu_baseline(args, net_global, x_const):
     return out
 
 
+def setup_split(args, net, rank, world, dist, dev, T):
+    """C5 at N > 1: the largest outlet basin routed by a group of ranks (ddr_amd.split) when it exceeds
+    twice a rank's share, the other basins LPT-sharded over the remaining ranks.  A short hand-shake
+    launch checks the cross-rank path on this machine; if any rank fails it, every rank falls back to
+    whole-basin sharding (returns None; so does a plan without a split).  DDR_SPLIT_BASIN=0 disables, =force splits even at N = 2."""
+    from ddr_amd.split import SplitBasin, plan_block_ranks, plan_ranks, sub_network
+
+    plan = plan_ranks(net.n, net.rows, net.cols, world, force=os.environ.get("DDR_SPLIT_BASIN") == "force")
+    ids_r, sp = plan[rank]
+    any_split = any(s is not None for _, s in plan)
+    if not any_split:
+        return None
+    n_loc, rows, cols, ids = sub_network(net.n, net.rows, net.cols, ids_r)
+    g = split = None
+    handle = None
+    if sp is not None:
+        group, idx = sp
+        k = len(group)
+        # k GPUs' worth of workgroups (one CU's share each); a one-GPU rehearsal (every rank on device 0)
+        # keeps the group's blocks within the one device so that all of them can be resident at once
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        wg = cus if os.environ.get("DDR_BENCH_SAME_DEVICE") == "1" else k * cus
+        g = RiverGraph(n_loc, rows, cols, steps_hint=T, target_blocks=wg, max_resident=wg)
+        nloc = np.zeros(g.info.n_blocks, dtype=np.int32)
+        _lib.check(_lib.load().ddr_graph_blocks(g.handle, nloc.ctypes.data, len(nloc)))
+        br = plan_block_ranks(nloc, k)
+
+        def exchange(obj):
+            res = [None] * world
+            dist.all_gather_object(res, (rank, obj))
+            return [o for r_, o in res if r_ in group]
+
+        split = SplitBasin(g, br, idx, k, T, exchange)
+    else:
+        res = [None] * world
+        dist.all_gather_object(res, (rank, handle))  # the split group's handle exchange (nothing to share)
+    ok = torch.ones(1, device=dev)
+    if split is not None:
+        try:  # hand-shake: a short forward on the split graph, every cross-rank edge exercised
+            from ddr_amd.ops import check_status
+
+            Th = min(T, 48)
+            z = torch.full((n_loc,), 0.5, device=dev)
+            route(g, torch.full((Th, n_loc), 0.1, device=dev), z * 0.1, z, z * 10, z * 1000 + 1000, z * 0.01, z * 0.5,
+                  save=False, steps=Th)
+            check_status()
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            log(f"[rank {rank}] split-basin hand-shake failed ({e}); falling back to whole-basin sharding")
+            ok.zero_()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if ok.item() < 1:
+        if split is not None:
+            g.close()
+            split.close()
+        return None
+    return g, split, n_loc, rows, cols, ids
+
+
 def counter_file(args, lib_hash):
     """PMC summary of this workload for the loaded library build (profiles/, made by tools/pmc.sh +
     tools/pmc_to_json.py); None when absent or stale (another build or configuration)."""
@@ -266,8 +325,17 @@ def main():
     # this rank's outlet basins (LPT by reach count, distributed.shard_network; all of them at N = 1)
     n_loc, rows, cols, ids = shard_network(net.n, net.rows, net.cols, rank, world) if world > 1 else (
         net.n, net.rows, net.cols, np.arange(net.n))
-    g = RiverGraph(n_loc, rows, cols, steps_hint=T)
-    log(f"[rank {rank}] {g} built in {time.perf_counter() - t_setup:.1f}s")
+    g, split = None, None
+    if args.workload == "c5" and world > 1 and not alone and os.environ.get("DDR_SPLIT_BASIN", "1") != "0":
+        plan = setup_split(args, net, rank, world, dist, dev, T)
+        if plan is not None:
+            g, split, n_loc, rows, cols, ids = plan
+    if g is None:
+        g = RiverGraph(n_loc, rows, cols, steps_hint=T)
+    log(f"[rank {rank}] {g} built in {time.perf_counter() - t_setup:.1f}s"
+        + (f", split basin rank {split.index}/{split.k} ({len(split.owned_reaches)} reaches, {split.n_x} cross-rank cut edges)"
+           if split else ""))
+    n_owned = n_loc if split is None else len(split.owned_reaches)
     at = synthetic.reach_attributes(net.n, 11, x_const=x_const)
     u = synthetic.unit_parameters(net.n, 11)
     tt = lambda a: torch.from_numpy(np.ascontiguousarray(np.asarray(a)[ids])).to(dev)  # noqa: E731
@@ -385,7 +453,7 @@ def main():
 
     # ---- reductions over ranks ------------------------------------------------------------------------
     sizes = torch.zeros(max(world, 1), device=dev, dtype=torch.float64)
-    sizes[rank] = n_loc
+    sizes[rank] = n_owned
     tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(sizes, op=dist.ReduceOp.SUM)
@@ -397,7 +465,7 @@ def main():
 
     if rank == 0 or alone:
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-        reach_steps = n_loc * (T - 1)
+        reach_steps = n_owned * (T - 1)
         kern = {}
         for key, nb in (("forward", fwd_bytes), ("backward", bwd_bytes)):
             if kms[key]:
@@ -440,7 +508,10 @@ def main():
                        "basins": int(len(net.basin_sizes)), "largest_basin": largest,
                        "max_depth_rank0": g.info.max_depth, "blocks_rank0": g.info.n_blocks,
                        "cut_edges_rank0": g.info.n_cut, "generations_rank0": g.info.generations,
-                       "parallelism": f"outlet basins LPT-sharded over {world} GPU(s)",
+                       "parallelism": f"outlet basins LPT-sharded over {world} GPU(s)" + (
+                           f"; the largest basin split over ranks 0..{split.k - 1} (ddr_amd.split)" if split else ""),
+                       "split_basin": None if split is None else {"ranks": split.k, "cross_cut_edges": split.n_x,
+                                                                  "receive_memory_kind": split.kind},
                        "reaches_per_rank": [int(s) for s in sizes],
                        "load_max_over_mean": float(sizes.max() / sizes.mean()),
                        "basin_bound_speedup": float(total_reaches / max(sizes.max(), largest))},

@@ -115,6 +115,13 @@ _SIGS = {
     "ddr_geometry_stats_f32": (C.c_int, [_P, _I64, _I64, _I64, _I64, _P, _P, _I64, _P, _P, C.c_double, C.c_double,
                                          _P, _P]),
     "ddr_graph_status": (C.c_int, [_P, _P]),
+    "ddr_xmem_alloc": (C.c_int, [_I64, C.POINTER(C.c_void_p), _P, C.POINTER(C.c_int32)]),
+    "ddr_xmem_open": (C.c_int, [_P, C.POINTER(C.c_void_p)]),
+    "ddr_xmem_close": (C.c_int, [_P, _I32]),
+    "ddr_xmem_bytes": (C.c_int, [_I64, _I64, C.POINTER(C.c_int64)]),
+    "ddr_graph_blocks": (C.c_int, [_P, _P, _I64]),
+    "ddr_graph_cut_blocks": (C.c_int, [_P, _P, _P, _I64]),
+    "ddr_graph_set_split": (C.c_int, [_P, _I32, _I32, _P, _P, _P, _I64, C.POINTER(C.c_int64)]),
     "ddr_status_check": (C.c_int, [_I32]),
     "ddr_set_debug_flags": (C.c_int, [_I32]),
     "ddr_tri_solve": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _P]),

@@ -191,6 +191,43 @@ ddr_status check_launchable(const Graph* g, bool backward) {
   return DDR_OK;
 }
 
+// Split basin (SplitState): the launch's split arguments, its receive rows reset, and the epoch hand-shake
+// with the other ranks of the split (slot 0: forward, 1: backward), all stream-ordered before the launch.
+ddr_status split_prepare(const Graph* g, RouteArgs& a, int64_t T, int slot, hipStream_t s) {
+  SplitState& sp = const_cast<Graph*>(g)->split;
+  if (sp.nranks == 0) return DDR_OK;
+  if (T > sp.t_cap) return fail(DDR_ERR_ARG, "split basin: T exceeds the receive rows' capacity (ddr_graph_set_split t_cap)");
+  a.owned = sp.owned;
+  a.xid = sp.xid;
+  a.xcons = sp.xcons;
+  a.xprod = sp.xprod;
+  auto rows = [&](char* base, int which) {
+    double* f = reinterpret_cast<double*>(base + xmem_flags_bytes());
+    return which == 0 ? f : f + sp.n_x * T;
+  };
+  a.xfwd = rows(sp.local, 0);
+  a.xbwd = rows(sp.local, 1);
+  SplitBarrierArgs b;
+  std::memset(&b, 0, sizeof(b));
+  for (int p = 0; p < sp.nranks; ++p) {
+    a.pxfwd[p] = rows(sp.peers[p], 0);
+    a.pxbwd[p] = rows(sp.peers[p], 1);
+    b.peer[p] = reinterpret_cast<unsigned long long*>(sp.peers[p]);
+  }
+  if (sp.n_x > 0) {
+    double* mine = slot == 0 ? a.xfwd : a.xbwd;
+    DDR_HIP(hipMemsetAsync(mine, 0xFF, sizeof(double) * (size_t)(sp.n_x * T) * (slot == 0 ? 1 : 2), s));
+  }
+  b.mine = reinterpret_cast<unsigned long long*>(sp.local);
+  b.rank = sp.rank;
+  b.nranks = sp.nranks;
+  b.slot = slot;
+  b.epoch = ++sp.epoch[slot];
+  b.status = a.status;
+  DDR_HIP(launch_split_barrier(b, s));
+  return DDR_OK;
+}
+
 template <typename R>
 ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, const R* qprime,
                         int64_t T, const R* q0, R* runoff, R* x_save, double* bnd, void* status, R* q_last,
@@ -223,6 +260,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   a.ss_last = ss;
   a.prof = g_prof[0];
   a.qs = x_save + (g->n * T + g->sum_dn);
+  if ((st = split_prepare(g, a, T, 0, s))) return st;
   DDR_HIP(launch_gather_qprime<R>(g, a, s));
   DDR_HIP(timing_mark(0, 0, s));
   DDR_HIP(launch_route<R>(g, a, false, s));
@@ -256,6 +294,8 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   if (flags & DDR_FWD_ACCUMULATE) return fail(DDR_ERR_ARG, "DDR_FWD_ACCUMULATE launches have no adjoint");
   if (gauges && (!gauges->reach_offsets || !gauges->reach_gauges))
     return fail(DDR_ERR_ARG, "gauge mode backward needs the reach->gauge map");
+  if (g->split.nranks > 0 && (gauges || gqp || gq0))
+    return fail(DDR_ERR_ARG, "split basin: gauge mode and state gradients are not supported");
   const bool state = gqp || gq0;
   if (state) {
     if (!work) return fail(DDR_ERR_ARG, "state gradients need the workspace (ddr_state_work_bytes)");
@@ -297,6 +337,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
       a.gmask0 = mask;
     }
   }
+  if ((st = split_prepare(g, a, T, 1, s))) return st;
   DDR_HIP(timing_mark(1, 0, s));
   DDR_HIP(launch_route<R>(g, a, true, s));
   DDR_HIP(timing_mark(1, 1, s));
@@ -503,6 +544,144 @@ ddr_status ddr_graph_destroy(ddr_graph* g) {
 ddr_status ddr_graph_destroy_async(ddr_graph* g, void* stream) {
   DDR_GUARD({
     destroy_graph(reinterpret_cast<Graph*>(g), static_cast<hipStream_t>(stream));
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_xmem_alloc(int64_t bytes, void** ptr, void* handle, int32_t* kind) {
+  DDR_GUARD({
+    if (bytes <= 0 || !ptr || !handle) return fail(DDR_ERR_ARG, "bad ddr_xmem_alloc arguments");
+    // uncached device memory (no stale L2 copy of a peer's stores); fine-grained, then plain device
+    // memory where the uncached kind cannot be exported
+    for (int k = 0; k < 3; ++k) {
+      const unsigned flag = k == 0 ? hipDeviceMallocUncached : (k == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocDefault);
+      void* p = nullptr;
+      if (hipExtMallocWithFlags(&p, (size_t)bytes, flag) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
+      hipIpcMemHandle_t h;
+      if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        continue;
+      }
+      DDR_HIP(hipMemset(p, 0, (size_t)bytes));
+      std::memcpy(handle, &h, sizeof(h));
+      *ptr = p;
+      if (kind) *kind = k;
+      return DDR_OK;
+    }
+    return fail(DDR_ERR_HIP, "ddr_xmem_alloc: no exportable device allocation");
+  })
+}
+
+ddr_status ddr_xmem_open(const void* handle, void** ptr) {
+  DDR_GUARD({
+    if (!handle || !ptr) return fail(DDR_ERR_ARG, "null argument");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle, sizeof(h));
+    DDR_HIP(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_xmem_close(void* ptr, int32_t opened) {
+  DDR_GUARD({
+    if (!ptr) return DDR_OK;
+    DDR_HIP(opened ? hipIpcCloseMemHandle(ptr) : hipFree(ptr));
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_xmem_bytes(int64_t n_x, int64_t T, int64_t* bytes) {
+  if (n_x < 0 || T < 1 || !bytes) return fail(DDR_ERR_ARG, "bad ddr_xmem_bytes arguments");
+  *bytes = (int64_t)xmem_bytes(n_x, T);
+  return DDR_OK;
+}
+
+ddr_status ddr_graph_blocks(const ddr_graph* gh, int32_t* nloc, int64_t cap) {
+  if (!gh || !nloc) return fail(DDR_ERR_ARG, "null argument");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (cap < (int64_t)g->blocks.size()) return fail(DDR_ERR_ARG, "ddr_graph_blocks: capacity below n_blocks");
+  for (size_t b = 0; b < g->blocks.size(); ++b) nloc[b] = g->blocks[b].nloc;
+  return DDR_OK;
+}
+
+ddr_status ddr_graph_cut_blocks(const ddr_graph* gh, int32_t* prod, int32_t* cons, int64_t cap) {
+  DDR_GUARD({
+    if (!gh || !prod || !cons) return fail(DDR_ERR_ARG, "null argument");
+    const Graph* g = reinterpret_cast<const Graph*>(gh);
+    if (cap < g->n_cut) return fail(DDR_ERR_ARG, "ddr_graph_cut_blocks: capacity below n_cut");
+    HostSchedule H;
+    if (g->uploaded) {
+      ddr_status st = device_schedule_to_host(g, H);
+      if (st) return st;
+    } else {
+      H = g->hs;
+    }
+    for (int64_t e = 0; e < g->n_cut; ++e) prod[e] = cons[e] = -1;
+    for (size_t b = 0; b < g->blocks.size(); ++b) {
+      const BlockDesc& B = g->blocks[b];
+      for (int i = 0; i < B.nloc; ++i) {
+        const int32_t e = H.cut[B.pos0 + i];
+        if (e >= 0) prod[e] = (int32_t)b;
+      }
+      for (int v = 0; v < B.nvirt; ++v) cons[H.v_edge[B.virt0 + v]] = (int32_t)b;
+    }
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_graph_set_split(ddr_graph* gh, int32_t rank, int32_t nranks, const int32_t* block_rank, void* local,
+                               void* const* peers, int64_t t_cap, int64_t* n_x_out) {
+  DDR_GUARD({
+    if (!gh || !block_rank || !local || !peers || t_cap < 1) return fail(DDR_ERR_ARG, "bad ddr_graph_set_split arguments");
+    if (nranks < 2 || nranks > kMaxSplitRanks || rank < 0 || rank >= nranks)
+      return fail(DDR_ERR_ARG, "split basin: 2 <= nranks <= 16, 0 <= rank < nranks");
+    Graph* g = reinterpret_cast<Graph*>(gh);
+    if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
+    if (g->split.nranks > 0) return fail(DDR_ERR_ARG, "split basin: already set");
+    const int64_t nb = (int64_t)g->blocks.size();
+    for (int64_t b = 0; b < nb; ++b)
+      if (block_rank[b] < 0 || block_rank[b] >= nranks) return fail(DDR_ERR_ARG, "split basin: block rank out of range");
+    std::vector<int32_t> prod((size_t)g->n_cut);
+    std::vector<int32_t> cons((size_t)g->n_cut);
+    ddr_status st = ddr_graph_cut_blocks(gh, prod.data(), cons.data(), g->n_cut);
+    if (st) return st;
+    std::vector<int32_t> xid((size_t)g->n_cut);
+    std::fill(xid.begin(), xid.end(), -1);
+    std::vector<int32_t> xcons;
+    std::vector<int32_t> xprod;
+    for (int64_t e = 0; e < g->n_cut; ++e) {
+      if (prod[e] < 0 || cons[e] < 0) return fail(DDR_ERR_ARG, "split basin: cut edge without both blocks");
+      if (block_rank[prod[e]] != block_rank[cons[e]]) {
+        xid[e] = (int32_t)xcons.size();
+        xcons.push_back(block_rank[cons[e]]);
+        xprod.push_back(block_rank[prod[e]]);
+      }
+    }
+    std::vector<uint8_t> owned(nb);
+    for (int64_t b = 0; b < nb; ++b) owned[b] = block_rank[b] == rank ? 1 : 0;
+    auto up = [&](const void* src, size_t bytes, void** dst) -> hipError_t {
+      hipError_t e = hipMalloc(dst, bytes < 16 ? 16 : bytes);
+      if (e != hipSuccess) return e;
+      g->allocations.push_back(*dst);
+      return bytes ? hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+    };
+    SplitState sp;
+    DDR_HIP(up(owned.data(), owned.size(), reinterpret_cast<void**>(&sp.owned)));
+    DDR_HIP(up(xid.data(), xid.size() * 4, reinterpret_cast<void**>(&sp.xid)));
+    DDR_HIP(up(xcons.data(), xcons.size() * 4, reinterpret_cast<void**>(&sp.xcons)));
+    DDR_HIP(up(xprod.data(), xprod.size() * 4, reinterpret_cast<void**>(&sp.xprod)));
+    sp.rank = rank;
+    sp.nranks = nranks;
+    sp.n_x = (int32_t)xcons.size();
+    sp.t_cap = t_cap;
+    sp.local = static_cast<char*>(local);
+    for (int p = 0; p < nranks; ++p) sp.peers[p] = static_cast<char*>(peers[p]);
+    g->split = sp;
+    if (n_x_out) *n_x_out = sp.n_x;
     return DDR_OK;
   })
 }

@@ -130,6 +130,28 @@ struct DeviceViews {
   int32_t* block = nullptr;
 };
 
+// One basin's schedule shared by several ranks (ddr_graph_set_split): every rank builds the same
+// graph, runs the blocks it owns and skips the others; a cut edge between blocks of two ranks carries
+// its granules through the receive block of the rank that reads them (forward: the consumer block's
+// rank, backward: the producer's), written there with system-scope stores (ddr_xmem_alloc: uncached
+// device memory shared by IPC handles).  A receive block: [2][kMaxSplitRanks] u64 launch epochs
+// (forward, backward; set by each peer before its launch) | forward rows [n_x][T] f64 | backward rows
+// [n_x][T][2] f64.
+constexpr int kMaxSplitRanks = 16;
+struct SplitState {
+  int32_t rank = 0, nranks = 0, n_x = 0;
+  int64_t t_cap = 0;
+  uint8_t* owned = nullptr;  // device (n_blocks): 1 = this rank runs the logical block
+  int32_t* xid = nullptr;    // device (n_cut): index among the cross-rank cut edges, -1 = local
+  int32_t* xcons = nullptr;  // device (n_x): rank of the consumer (downstream) block
+  int32_t* xprod = nullptr;  // device (n_x): rank of the producer (upstream) block
+  char* local = nullptr;     // this rank's receive block
+  char* peers[kMaxSplitRanks] = {};
+  unsigned long long epoch[2] = {0, 0};
+};
+inline size_t xmem_flags_bytes() { return 2 * kMaxSplitRanks * sizeof(unsigned long long); }
+inline size_t xmem_bytes(int64_t n_x, int64_t T) { return xmem_flags_bytes() + (size_t)(n_x * T) * 24; }
+
 struct Graph {
   int64_t n = 0, nnz = 0;
   std::vector<int64_t> crow, col;
@@ -155,6 +177,7 @@ struct Graph {
   void* staging = nullptr;     // pinned host sources of the device build's last uploads
   std::vector<void*> allocations;        // hipMalloc (host builds)
   std::vector<void*> async_allocations;  // device_get blocks (device builds): returned stream-ordered
+  SplitState split;                      // ddr_graph_set_split (nranks == 0: not split)
 };
 
 // ---- piece-level packing, shared by the host builder (graph.cpp) and the device builder ---------

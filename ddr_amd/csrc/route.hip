@@ -75,6 +75,16 @@ __device__ __forceinline__ unsigned long long load_granule(const double* p) {
   return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
+// Cross-rank granules (split basin): system scope, so a peer GPU's stores into this rank's receive
+// rows and this rank's stores into a peer's are seen through neither side's L2
+__device__ __forceinline__ void store_granule_sys(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long load_granule_sys(const double* p) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Spin until the granules of a chunk are published (bounded).  On a timeout (or with the debug flag
 // that forces one) record it in the status block and return NaN: the corruption then shows in the
@@ -84,21 +94,27 @@ constexpr int kImportBatch = 4;
 // Batched form for the chunk imports: the granules row[t0 + s * stride] (s < C; outside [lo, hi):
 // 0) are all requested before the first wait, so a chunk costs one memory round trip, not C; only
 // the still-unpublished ones are polled again.
-template <int C>
+template <int C, bool Sys = false>
 __device__ __forceinline__ void wait_granules(const double* row, int64_t t0, int stride, int64_t lo, int64_t hi,
                                               double (&out)[C], unsigned* status, int bid, bool force_timeout) {
+  auto ld = [](const double* p) { return Sys ? load_granule_sys(p) : load_granule(p); };
   unsigned long long v[C];
   unsigned pend = 0;
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     const int64_t t = t0 + (int64_t)s * stride;
-    v[s] = (t >= lo && t < hi) ? load_granule(row + t) : 0ull;  // +0.0 outside the window
+    v[s] = (t >= lo && t < hi) ? ld(row + t) : 0ull;  // +0.0 outside the window
   }
 #pragma unroll
   for (int s = 0; s < C; ++s) pend |= (v[s] == kSentinel ? 1u : 0u) << s;
   unsigned spins = 0;
   while (pend != 0u || force_timeout) {
-    if (force_timeout || ++spins > (1u << 24)) {
+    ++spins;
+    // a hand-off already failed in this launch (e.g. a split-basin peer that never arrives): give up
+    // at once instead of spinning out every later wait too
+    const bool failed = (spins & 1023u) == 0u &&
+                        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    if (force_timeout || failed || spins > (1u << 24)) {
       atomicAdd(status, 1u);
       atomicCAS(status + 1, 0u, (unsigned)bid + 1u);
 #pragma unroll
@@ -112,7 +128,7 @@ __device__ __forceinline__ void wait_granules(const double* row, int64_t t0, int
     __builtin_amdgcn_s_sleep(2);
 #pragma unroll
     for (int s = 0; s < C; ++s) {
-      const unsigned long long w = ((pend >> s) & 1u) ? load_granule(row + (t0 + (int64_t)s * stride)) : v[s];
+      const unsigned long long w = ((pend >> s) & 1u) ? ld(row + (t0 + (int64_t)s * stride)) : v[s];
       v[s] = w;
       pend &= ~((w != kSentinel ? 1u : 0u) << s);
     }
@@ -368,6 +384,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   constexpr int NP = KR < NPW ? KR : NPW;  // slices whose physics runs in lockstep
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bid = take_ticket(a.status, kStatusTicketFwd, a.nblocks, false, reinterpret_cast<int*>(smem));
+  if (a.owned && !a.owned[bid]) return;  // split basin: another rank's block
   const BlockDesc B = block_desc(a.s.blocks, bid);
   const int tid = threadIdx.x;
   // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
@@ -489,13 +506,26 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // thread requests the kChunkFwd granules at once
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
       if (vown) {
+        // split basin: a cut edge from another rank's block arrives in this rank's receive rows
+        const int xi = a.xid ? a.xid[v_edge] : -1;
+        if (xi >= 0) {
 #pragma unroll
-        for (int h = 0; h < kChunkFwd; h += kImportBatch) {
-          double g[kImportBatch];
-          wait_granules<kImportBatch>(a.bnd + (int64_t)v_edge * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status, bid,
-                                      force_to);
+          for (int h = 0; h < kChunkFwd; h += kImportBatch) {
+            double g[kImportBatch];
+            wait_granules<kImportBatch, true>(a.xfwd + (int64_t)xi * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status,
+                                              bid, force_to);
 #pragma unroll
-          for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunkFwd + h + i] = g[i];
+            for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunkFwd + h + i] = g[i];
+          }
+        } else {
+#pragma unroll
+          for (int h = 0; h < kChunkFwd; h += kImportBatch) {
+            double g[kImportBatch];
+            wait_granules<kImportBatch>(a.bnd + (int64_t)v_edge * T, (int64_t)tau - v_off + h, 1, 0, T, g, a.status,
+                                        bid, force_to);
+#pragma unroll
+            for (int i = 0; i < kImportBatch; ++i) ring[vi * kChunkFwd + h + i] = g[i];
+          }
         }
       }
 #ifndef DDR_FWD_IMPORT_BARRIER
@@ -609,7 +639,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
-          if (B.ncout > 0 && (off[k] >> 16)) store_granule(a.bnd + (int64_t)(B.cout0 + (off[k] >> 16) - 1) * T + t, x);
+          if (B.ncout > 0 && (off[k] >> 16)) {
+            const int64_t e = B.cout0 + (off[k] >> 16) - 1;
+            const int xi = a.xid ? a.xid[e] : -1;  // split basin: the consumer block is another rank's
+            if (xi >= 0) store_granule_sys(a.pxfwd[a.xcons[xi]] + (int64_t)xi * T + t, x);
+            else store_granule(a.bnd + e * T + t, x);
+          }
           // (the last step's Q, top width and side slope: route_last_kernel, from the saved states --
           // no rarely taken stores, and no pointers held across the tick loop for them)
           Q[k] = Qn;
@@ -762,6 +797,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   constexpr int BS = kBlockThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bid = take_ticket(a.status, kStatusTicketBwd, a.nblocks, true, reinterpret_cast<int*>(smem));
+  if (a.owned && !a.owned[bid]) return;  // split basin: another rank's block
   const BlockDesc B = block_desc(a.s.blocks, bid);
   const int tid = threadIdx.x;
   // first lane of this wave (scalar): waves with no reach in slice k skip it (scalar branch),
@@ -869,8 +905,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
   // x of a virtual inflow (the upstream reach of cut edge v_edge) at step t, from the forward's
   // boundary granules (t clamped into [0, T))
+  const int vxi = (vown && a.xid) ? a.xid[v_edge] : -1;  // split basin: the virtual's cross-rank row
   auto load_virt = [&](int64_t t) -> double {
     const int64_t tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
+    if (vxi >= 0) return __longlong_as_double(load_granule_sys(a.xfwd + (int64_t)vxi * T + tc));
     return a.bnd[(int64_t)v_edge * T + tc];
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
@@ -957,7 +995,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         R A = R(0), Bv = R(0);
         if (t >= tmin && t < T) {
           double g[2];
-          wait_granules<2>(a.bwd_bnd + ((int64_t)(B.cout0 + c) * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
+          const int xi = a.xid ? a.xid[B.cout0 + c] : -1;  // split basin: the consumer is another rank's block
+          if (xi >= 0) wait_granules<2, true>(a.xbwd + ((int64_t)xi * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
+          else wait_granules<2>(a.bwd_bnd + ((int64_t)(B.cout0 + c) * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
           A = R(g[0]);
           Bv = R(g[1]);
         }
@@ -976,8 +1016,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int t = tau - v_off;
       if (t >= tmin && t < T) {
         const int dloc = v_dloc_of();
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
-        store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
+        if (vxi >= 0) {  // split basin: the producer block is another rank's
+          double* dst = a.pxbwd[a.xprod[vxi]] + ((int64_t)vxi * T + t) * 2;
+          store_granule_sys(dst, (double)sa[dloc]);
+          store_granule_sys(dst + 1, (double)sb[dloc]);
+        } else {
+          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
+          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
+        }
       }
       sx[B.nloc + tid] = R(vxc);
     }
@@ -1235,6 +1281,7 @@ template <typename R, int G>
 __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
   R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
+  if (a.owned && !a.owned[blockIdx.x]) return;  // split basin: another rank's block
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int64_t T = a.T, N = a.N;
   const int64_t t0 = (int64_t)blockIdx.y * G;
@@ -1319,6 +1366,7 @@ template <typename R, int G>
 __global__ void __launch_bounds__(1024) gather_qprime_rows_kernel(RouteArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
   R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
+  if (a.owned && !a.owned[blockIdx.x]) return;  // split basin: another rank's block
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int64_t N = a.N, d0 = (int64_t)blockIdx.y * G;
   const int nl = B.nloc;
@@ -1519,6 +1567,37 @@ int max_resident_blocks(const Graph* g, bool backward) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, g->device) != hipSuccess) return -1;
   return nb * prop.multiProcessorCount;
+}
+
+// Split basin: before a routing launch, every rank of the split announces (system-scope store into each
+// peer's epoch word) that its receive rows are reset for launch `epoch` and waits until every peer has
+// announced the same; only then may a peer's blocks write into them.  Bounded: a peer that never
+// arrives is recorded in the status block (DDR_ERR_TIMEOUT at the next library call).
+__global__ void split_barrier_kernel(SplitBarrierArgs b) {
+  if (threadIdx.x != 0) return;
+  for (int p = 0; p < b.nranks; ++p) {
+    if (p == b.rank) continue;
+    __hip_atomic_store(b.peer[p] + b.slot * kMaxSplitRanks + b.rank, b.epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (int p = 0; p < b.nranks; ++p) {
+    if (p == b.rank) continue;
+    unsigned spins = 0;
+    while (__hip_atomic_load(b.mine + b.slot * kMaxSplitRanks + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
+           b.epoch) {
+      if (++spins > (1u << 24)) {
+        atomicAdd(b.status, 1u);
+        atomicCAS(b.status + 1, 0u, 0x40000000u + (unsigned)p);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+}
+
+hipError_t launch_split_barrier(const SplitBarrierArgs& b, hipStream_t stream) {
+  hipLaunchKernelGGL(split_barrier_kernel, dim3(1), dim3(64), 0, stream, b);
+  return hipGetLastError();
 }
 
 template <typename R>

@@ -54,6 +54,16 @@ struct RouteArgs {
   void* gq0;
   const unsigned char* gmask0;
   unsigned long long* prof;  // debug per-workgroup profile (ddr_set_block_profile), or null
+  // split basin (SplitState, internal.h; null when not split): logical blocks of other ranks are
+  // skipped, cross-rank cut edges read this rank's receive rows and write the peer's
+  const uint8_t* owned;
+  const int32_t* xid;
+  const int32_t* xcons;
+  const int32_t* xprod;
+  double* xfwd;
+  double* xbwd;
+  double* pxfwd[kMaxSplitRanks];
+  double* pxbwd[kMaxSplitRanks];
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
   float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
   double ln_dlb;  // ln of the fp32-rounded depth lower bound (fp32 pow derivation, physics.h)
@@ -73,6 +83,15 @@ struct GaugeArgs {
 
 template <typename R>
 hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipStream_t stream);
+// split basin: the epoch hand-shake before a routing launch (route.hip: split_barrier_kernel)
+struct SplitBarrierArgs {
+  unsigned long long* mine;                  // this rank's epoch words ([2][kMaxSplitRanks])
+  unsigned long long* peer[kMaxSplitRanks];  // every rank's epoch words
+  int32_t rank, nranks, slot;                // slot 0: forward, 1: backward
+  unsigned long long epoch;
+  unsigned* status;
+};
+hipError_t launch_split_barrier(const SplitBarrierArgs& b, hipStream_t stream);
 // dL/dq' (rows of the caller's store, (rows, N)) from the state-gradient backward's gqs: the adjoint
 // of gather_qprime (sum over the steps reading each row, times flow_scale, 0 for a filled divide)
 template <typename R>

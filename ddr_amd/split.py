@@ -1,0 +1,144 @@
+"""One outlet basin routed by several GPUs (BASELINE.json north star item (5), SURVEY.md §8(e) "next").
+
+Sharding by outlet basin (``distributed.shard_network``) leaves a basin that is larger than a rank's
+share on one GPU: C5's 281k-reach basin (0.35 N) floors the 8-GPU step at its one-GPU time.  Here the
+ranks of a *split group* all build the same graph of that basin (the builders are deterministic) with
+k times the workgroups of one GPU, and each runs a contiguous range of its logical blocks (ticket
+order = piece-height order, balanced by reaches).  The time-pipelined hand-off between blocks is the
+same fp64 data-is-flag granule as inside one GPU; a cut edge whose two blocks belong to different
+ranks writes its granules into the receive memory of the rank that reads them (system-scope stores
+over xGMI into uncached memory exported by IPC handle, ``ddr_xmem_*``).  Before every routing launch
+the ranks reset their receive rows and hand-shake on the device (``include/ddr_mc.h``), so the
+training step needs no extra host synchronisation.
+
+The reference has no counterpart (its solve runs a basin on one device, ``routing/utils.py:515-692``).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .partition import basin_labels, extract_basins, shard_basins
+
+
+def plan_block_ranks(nloc, k: int) -> np.ndarray:
+    """Rank of each logical block: k contiguous ranges of the ticket order with equal reach counts."""
+    nloc = np.asarray(nloc, dtype=np.int64)
+    if k < 1 or len(nloc) < k:
+        raise ValueError("need at least one block per rank")
+    mid = np.cumsum(nloc) - nloc / 2.0
+    r = np.minimum((mid * k / max(float(nloc.sum()), 1.0)).astype(np.int64), k - 1)
+    # every rank gets at least one block (tiny graphs)
+    for i in range(k):
+        if not np.any(r == i):
+            r[min(i, len(r) - 1)] = i
+    return np.maximum.accumulate(r).astype(np.int32)
+
+
+def plan_ranks(n: int, rows, cols, world: int, factor: float = 2.0, force: bool = False):
+    """Per rank: (reach_ids, split) where split is None (whole basins, LPT over the ranks outside the
+    split group) or (group_ranks, index_in_group) for the ranks that route the largest basin together.
+
+    The largest basin is split when it exceeds ``factor`` x the per-rank mean (or ``force``) and at
+    least one rank remains for the other basins; its group has k = round(size / mean) ranks.  ``force``
+    with two ranks (a rehearsal) splits the largest basin over both and leaves the other basins out."""
+    lab = basin_labels(n, rows, cols)
+    outlets, inv, sizes = np.unique(lab, return_inverse=True, return_counts=True)
+    mean = n / max(world, 1)
+    big = int(np.argmax(sizes))
+    k = int(round(sizes[big] / mean)) if world > 1 else 0
+    k = min(max(k, 2), world - 1) if world > 2 else (2 if force and world == 2 else 0)
+    split = world > 1 and k >= 2 and (force or sizes[big] > factor * mean) and (world - k >= 1 or force)
+    out = []
+    if not split:
+        owner = np.empty(len(outlets), dtype=np.int64)
+        for r, idx in enumerate(shard_basins(sizes, world)):
+            owner[idx] = r
+        for r in range(world):
+            out.append((np.nonzero(owner[inv] == r)[0], None))
+        return out
+    group = list(range(k))
+    big_ids = np.nonzero(inv == big)[0]
+    rest = [i for i in range(len(outlets)) if i != big]
+    others = world - k
+    owner = np.full(len(outlets), -1, dtype=np.int64)
+    if others > 0 and rest:  # (none left: a forced 2-rank rehearsal routes only the split basin)
+        for j, idx in enumerate(shard_basins(sizes[rest], others)):
+            owner[np.asarray(rest)[idx]] = k + j
+    for r in range(world):
+        if r < k:
+            out.append((big_ids, (group, r)))
+        else:
+            out.append((np.nonzero(owner[inv] == r)[0], None))
+    return out
+
+
+def sub_network(n: int, rows, cols, ids):
+    keep = np.zeros(n, dtype=bool)
+    keep[ids] = True
+    return extract_basins(n, rows, cols, keep)
+
+
+class SplitBasin:
+    """Attach a split to ``graph`` (a RiverGraph built identically on every rank of the group).
+
+    ``exchange(obj) -> list`` gathers one picklable object from every rank of the group, in group
+    order (e.g. ``torch.distributed.all_gather_object`` restricted to the group)."""
+
+    def __init__(self, graph, block_rank, index: int, k: int, t_cap: int, exchange):
+        lib = _lib.load()
+        self.graph, self.k, self.index = graph, k, index
+        info = graph.info
+        self.block_rank = np.ascontiguousarray(block_rank, dtype=np.int32)
+        if len(self.block_rank) != info.n_blocks:
+            raise ValueError("block_rank needs one entry per logical block")
+        prod = np.empty(max(info.n_cut, 1), dtype=np.int32)
+        cons = np.empty(max(info.n_cut, 1), dtype=np.int32)
+        _lib.check(lib.ddr_graph_cut_blocks(graph.handle, prod.ctypes.data, cons.ctypes.data, int(info.n_cut)))
+        prod, cons = prod[:info.n_cut], cons[:info.n_cut]
+        self.n_x = int(np.count_nonzero(self.block_rank[prod] != self.block_rank[cons]))
+        nb = C.c_int64()
+        _lib.check(lib.ddr_xmem_bytes(self.n_x, int(t_cap), C.byref(nb)))
+        self.bytes = nb.value
+        ptr = C.c_void_p()
+        handle = (C.c_ubyte * 64)()
+        kind = C.c_int32()
+        _lib.check(lib.ddr_xmem_alloc(self.bytes, C.byref(ptr), handle, C.byref(kind)))
+        self.local, self.kind = ptr.value, kind.value
+        handles = exchange(bytes(handle))
+        if len(handles) != k:
+            raise ValueError("exchange must return one handle per rank of the group")
+        self.peers, self._opened = [], []
+        for r, h in enumerate(handles):
+            if r == index:
+                self.peers.append(self.local)
+                continue
+            p = C.c_void_p()
+            _lib.check(lib.ddr_xmem_open((C.c_ubyte * 64).from_buffer_copy(h), C.byref(p)))
+            self.peers.append(p.value)
+            self._opened.append(p.value)
+        arr = (C.c_void_p * k)(*self.peers)
+        n_x = C.c_int64()
+        _lib.check(lib.ddr_graph_set_split(graph.handle, index, k, self.block_rank.ctypes.data, self.local, arr,
+                                           int(t_cap), C.byref(n_x)))
+        if n_x.value != self.n_x:
+            raise RuntimeError("cross-rank cut edges disagree between the host plan and the library")
+        # the reaches this rank routes (their outputs and gradients are this rank's)
+        blk = graph.structure()["block"] if hasattr(graph, "structure") else None
+        self.owned_reaches = None if blk is None else np.nonzero(self.block_rank[blk] == index)[0]
+
+    def close(self) -> None:
+        """Release the receive memory (after the device is done with every launch of the split)."""
+        import torch
+
+        lib = _lib.load()
+        torch.cuda.synchronize()
+        for p in self._opened:
+            _lib.check(lib.ddr_xmem_close(p, 1))
+        self._opened = []
+        if self.local:
+            _lib.check(lib.ddr_xmem_close(self.local, 0))
+            self.local = None

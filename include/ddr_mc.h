@@ -329,6 +329,36 @@ ddr_status ddr_graph_status(const void* status, void* stream);
  * (whose outputs hold NaN).  wait = 1 blocks until every queued copy has landed.  No reference
  * counterpart (the reference solver raises ValueError on failure, routing/utils.py:598-600). */
 ddr_status ddr_status_check(int32_t wait);
+/* ---- One basin split across GPUs (no reference counterpart: the reference routes a basin on one
+ * device; north star item (5)) ----------------------------------------------------
+ * Every rank of a split builds the SAME graph of the basin (same COO and options: the builders are
+ * deterministic), then ddr_graph_set_split tells it which logical blocks it runs (block_rank[b] ==
+ * rank; the others are skipped).  A cut edge between blocks of two ranks carries its fp64 granules
+ * through the receive memory of the rank that reads them: the consumer's in the forward, the
+ * producer's in the backward, written with system-scope stores over xGMI.  Each rank allocates its
+ * receive memory with ddr_xmem_alloc (uncached device memory, exported as an IPC handle of
+ * DDR_XMEM_HANDLE_BYTES bytes), the ranks exchange handles (torch.distributed) and open the peers'
+ * with ddr_xmem_open.  Before each routing launch the ranks reset their receive rows and hand-shake
+ * on the device (an epoch word per peer), so no host synchronisation is needed; all ranks of a split
+ * must call forward / backward the same number of times with the same T.  Gauge mode and state
+ * gradients are not supported on a split graph. */
+enum { DDR_XMEM_HANDLE_BYTES = 64 };
+/* bytes of one rank's receive memory for n_x cross-rank cut edges and windows of up to T steps */
+ddr_status ddr_xmem_bytes(int64_t n_x, int64_t T, int64_t* bytes);
+/* kind: 0 uncached, 1 fine-grained, 2 plain device memory (the first kind that exports) */
+ddr_status ddr_xmem_alloc(int64_t bytes, void** ptr, void* handle, int32_t* kind);
+ddr_status ddr_xmem_open(const void* handle, void** ptr);
+ddr_status ddr_xmem_close(void* ptr, int32_t opened);
+/* reaches of every logical block (n_blocks entries, ticket order) */
+ddr_status ddr_graph_blocks(const ddr_graph* g, int32_t* nloc, int64_t cap);
+/* producer (upstream) and consumer (downstream) logical block of every cut edge (n_cut entries) */
+ddr_status ddr_graph_cut_blocks(const ddr_graph* g, int32_t* prod, int32_t* cons, int64_t cap);
+/* block_rank: n_blocks entries in [0, nranks); peers: every rank's receive memory (peers[rank] ==
+ * local), each ddr_xmem_bytes(n_x, t_cap) bytes, n_x = the cut edges whose blocks differ in rank
+ * (returned in *n_x) */
+ddr_status ddr_graph_set_split(ddr_graph* g, int32_t rank, int32_t nranks, const int32_t* block_rank, void* local,
+                               void* const* peers, int64_t t_cap, int64_t* n_x);
+
 /* Debug knobs.  DDR_DEBUG_FORCE_TIMEOUT: every inter-workgroup wait of the following launches
  * times out (tests the failure path).  DDR_DEBUG_NO_STEADY: the routing kernels run every tick
  * through their general path instead of the specialised steady-tick path (bitwise A/B; also set by

@@ -1,0 +1,60 @@
+"""A basin split across ranks (ddr_amd.split) routes bitwise like the same graph on one rank: two
+processes share cuda:0 (the one-GPU rehearsal; the receive memory goes through IPC handles and
+system-scope granules exactly as between GPUs), each runs half of the logical blocks, and the
+reaches each owns match the single-process launch bit for bit, forward and gradients, over two
+consecutive launches (the device hand-shake's epochs advance)."""
+
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import split_worker as W
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("math", ["exact", "faithful"])
+def test_split_basin_two_processes_bitwise(cuda, tmp_path, math):
+    from ddr_amd.graph import RiverGraph
+
+    net, at, u, qp, Wt = W.case()
+    g = RiverGraph(net.n, net.rows, net.cols, **W.GRAPH_KW)
+    assert g.info.n_blocks >= 4 and g.info.n_cut > 0
+    ref = W.route_once(g, net, at, u, qp, Wt, math, cuda)
+    port = _free_port()
+    outs = [str(tmp_path / f"r{r}.npz") for r in range(2)]
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), "2", str(port), outs[r],
+                               math], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=150)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            pytest.fail("split workers timed out")
+    assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
+    got = [np.load(o) for o in outs]
+    assert int(got[0]["fp"]) == int(got[1]["fp"]) == g.fingerprint()  # the same graph on every rank
+    assert int(got[0]["n_x"]) > 0  # the split really crosses ranks
+    owned = [d["owned"] for d in got]
+    assert len(np.intersect1d(owned[0], owned[1])) == 0 and len(owned[0]) + len(owned[1]) == net.n
+    for d, own in zip(got, owned):
+        for i in range(2):
+            assert np.array_equal(d[f"{i}_runoff"][own], ref["runoff"][own])
+            for k in ("g_n", "g_q_spatial", "g_p_spatial"):
+                assert np.array_equal(d[f"{i}_{k}"][own], ref[k][own]), k
