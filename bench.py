@@ -220,11 +220,16 @@ def setup_split(args, net, rank, world, dist, dev, T):
             dist.all_gather_object(res, (rank, obj))
             return [o for r_, o in res if r_ in group]
 
-        split = SplitBasin(g, br, idx, k, T, exchange)
+        ok = torch.ones(1, device=dev)
+        try:
+            split = SplitBasin(g, br, idx, k, T, exchange)
+        except Exception as e:  # noqa: BLE001  (the peers then fail the hand-shake below too)
+            log(f"[rank {rank}] split-basin setup failed ({e}); falling back to whole-basin sharding")
+            ok.zero_()
     else:
         res = [None] * world
         dist.all_gather_object(res, (rank, handle))  # the split group's handle exchange (nothing to share)
-    ok = torch.ones(1, device=dev)
+        ok = torch.ones(1, device=dev)
     if split is not None:
         try:  # hand-shake: a short forward on the split graph, every cross-rank edge exercised
             from ddr_amd.ops import check_status
@@ -240,8 +245,9 @@ def setup_split(args, net, rank, world, dist, dev, T):
             ok.zero_()
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if ok.item() < 1:
-        if split is not None:
+        if g is not None:
             g.close()
+        if split is not None:
             split.close()
         return None
     return g, split, n_loc, rows, cols, ids

@@ -1585,7 +1585,7 @@ __global__ void split_barrier_kernel(SplitBarrierArgs b) {
     unsigned spins = 0;
     while (__hip_atomic_load(b.mine + b.slot * kMaxSplitRanks + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) <
            b.epoch) {
-      if (++spins > (1u << 24)) {
+      if (++spins > (1u << 22)) {  // ~10 s
         atomicAdd(b.status, 1u);
         atomicCAS(b.status + 1, 0u, 0x40000000u + (unsigned)p);
         break;

@@ -106,12 +106,20 @@ class SplitBasin:
         ptr = C.c_void_p()
         handle = (C.c_ubyte * 64)()
         kind = C.c_int32()
-        _lib.check(lib.ddr_xmem_alloc(self.bytes, C.byref(ptr), handle, C.byref(kind)))
-        self.local, self.kind = ptr.value, kind.value
-        handles = exchange(bytes(handle))
+        self.local, self.peers, self._opened = None, [], []
+        err = None
+        try:
+            _lib.check(lib.ddr_xmem_alloc(self.bytes, C.byref(ptr), handle, C.byref(kind)))
+            self.local, self.kind = ptr.value, kind.value
+        except Exception as e:  # noqa: BLE001  (still take part in the exchange: the peers wait for it)
+            err = e
+        handles = exchange(None if err else bytes(handle))
+        if err is not None:
+            raise err
         if len(handles) != k:
             raise ValueError("exchange must return one handle per rank of the group")
-        self.peers, self._opened = [], []
+        if any(h is None for h in handles):
+            raise RuntimeError("split basin: a peer could not allocate its receive memory")
         for r, h in enumerate(handles):
             if r == index:
                 self.peers.append(self.local)

@@ -1,6 +1,6 @@
-"""A basin split across ranks (ddr_amd.split) routes bitwise like the same graph on one rank: two
-processes share cuda:0 (the one-GPU rehearsal; the receive memory goes through IPC handles and
-system-scope granules exactly as between GPUs), each runs half of the logical blocks, and the
+"""A basin split across ranks (ddr_amd.split) routes bitwise like the same graph on one rank: two or
+three processes share cuda:0 (the one-GPU rehearsal; the receive memory goes through IPC handles and
+system-scope granules exactly as between GPUs), each runs its range of the logical blocks, and the
 reaches each owns match the single-process launch bit for bit, forward and gradients, over two
 consecutive launches (the device hand-shake's epochs advance)."""
 
@@ -26,8 +26,8 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("math", ["exact", "faithful"])
-def test_split_basin_two_processes_bitwise(cuda, tmp_path, math):
+@pytest.mark.parametrize("math,world", [("exact", 2), ("faithful", 2), ("exact", 3)])
+def test_split_basin_processes_bitwise(cuda, tmp_path, math, world):
     from ddr_amd.graph import RiverGraph
 
     net, at, u, qp, Wt = W.case()
@@ -35,10 +35,11 @@ def test_split_basin_two_processes_bitwise(cuda, tmp_path, math):
     assert g.info.n_blocks >= 4 and g.info.n_cut > 0
     ref = W.route_once(g, net, at, u, qp, Wt, math, cuda)
     port = _free_port()
-    outs = [str(tmp_path / f"r{r}.npz") for r in range(2)]
+    outs = [str(tmp_path / f"r{r}.npz") for r in range(world)]
     env = dict(os.environ, PYTHONUNBUFFERED="1")
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), "2", str(port), outs[r],
-                               math], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "split_worker.py"), str(r), str(world), str(port),
+                               outs[r], math], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
     logs = []
     for p in procs:
         try:
@@ -49,10 +50,10 @@ def test_split_basin_two_processes_bitwise(cuda, tmp_path, math):
             pytest.fail("split workers timed out")
     assert all(p.returncode == 0 for p in procs), "\n".join(l[-3000:] for l in logs)
     got = [np.load(o) for o in outs]
-    assert int(got[0]["fp"]) == int(got[1]["fp"]) == g.fingerprint()  # the same graph on every rank
+    assert all(int(d["fp"]) == g.fingerprint() for d in got)  # the same graph on every rank
     assert int(got[0]["n_x"]) > 0  # the split really crosses ranks
     owned = [d["owned"] for d in got]
-    assert len(np.intersect1d(owned[0], owned[1])) == 0 and len(owned[0]) + len(owned[1]) == net.n
+    assert np.array_equal(np.sort(np.concatenate(owned)), np.arange(net.n))  # a partition of the reaches
     for d, own in zip(got, owned):
         for i in range(2):
             assert np.array_equal(d[f"{i}_runoff"][own], ref["runoff"][own])
