@@ -193,7 +193,7 @@ def setup_split(args, net, rank, world, dist, dev, T):
     twice a rank's share, the other basins LPT-sharded over the remaining ranks.  A short hand-shake
     launch checks the cross-rank path on this machine; if any rank fails it, every rank falls back to
     whole-basin sharding (returns None; so does a plan without a split).  DDR_SPLIT_BASIN=0 disables, =force splits even at N = 2."""
-    from ddr_amd.split import SplitBasin, plan_block_ranks, plan_ranks, sub_network
+    from ddr_amd.split import SplitBasin, block_edges, plan_block_ranks, plan_ranks, sub_network
 
     plan = plan_ranks(net.n, net.rows, net.cols, world, force=os.environ.get("DDR_SPLIT_BASIN") == "force")
     ids_r, sp = plan[rank]
@@ -211,9 +211,8 @@ def setup_split(args, net, rank, world, dist, dev, T):
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         wg = cus if os.environ.get("DDR_BENCH_SAME_DEVICE") == "1" else k * cus
         g = RiverGraph(n_loc, rows, cols, steps_hint=T, target_blocks=wg, max_resident=wg)
-        nloc = np.zeros(g.info.n_blocks, dtype=np.int32)
-        _lib.check(_lib.load().ddr_graph_blocks(g.handle, nloc.ctypes.data, len(nloc)))
-        br = plan_block_ranks(nloc, k)
+        nloc, prod, cons = block_edges(g)
+        br = plan_block_ranks(nloc, k, prod, cons)
 
         def exchange(obj):
             res = [None] * world
@@ -337,7 +336,10 @@ def main():
         if plan is not None:
             g, split, n_loc, rows, cols, ids = plan
     if g is None:
-        g = RiverGraph(n_loc, rows, cols, steps_hint=T)
+        # DDR_BENCH_TARGET_BLOCKS (prediction runs): pack this rank's network into that many workgroups,
+        # e.g. a split group's k x 256 blocks of the largest basin routed alone on one GPU as generations
+        tb = int(os.environ.get("DDR_BENCH_TARGET_BLOCKS", "0"))
+        g = RiverGraph(n_loc, rows, cols, steps_hint=T, target_blocks=tb, max_resident=tb)
     log(f"[rank {rank}] {g} built in {time.perf_counter() - t_setup:.1f}s"
         + (f", split basin rank {split.index}/{split.k} ({len(split.owned_reaches)} reaches, {split.n_x} cross-rank cut edges)"
            if split else ""))

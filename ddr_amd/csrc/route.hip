@@ -456,6 +456,15 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   load_math_tables();
   load_xlist(a, B, xl);
+  uintptr_t* xt = reinterpret_cast<uintptr_t*>(smem + a.xt_off);  // split: cut-outs' export rows
+  if (a.xt_off) {
+    for (int c = tid; c < B.ncout; c += BS) {
+      const int64_t e = B.cout0 + c;
+      const int xi = a.xid[e];
+      xt[c] = xi >= 0 ? (reinterpret_cast<uintptr_t>(a.pxfwd[a.xcons[xi]] + (int64_t)xi * T) | 1u)
+                      : reinterpret_cast<uintptr_t>(a.bnd + e * T);
+    }
+  }
   __syncthreads();
   unsigned long long prof_wait = 0;
   if (a.prof && tid == 0) prof_begin(a.prof, bid);
@@ -641,9 +650,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           }
           if (B.ncout > 0 && (off[k] >> 16)) {
             const int64_t e = B.cout0 + (off[k] >> 16) - 1;
-            const int xi = a.xid ? a.xid[e] : -1;  // split basin: the consumer block is another rank's
-            if (xi >= 0) store_granule_sys(a.pxfwd[a.xcons[xi]] + (int64_t)xi * T + t, x);
-            else store_granule(a.bnd + e * T + t, x);
+            if (a.xt_off) {  // split basin: the row from the block's table (another rank's: system scope)
+              const uintptr_t p = xt[(off[k] >> 16) - 1];
+              double* row = reinterpret_cast<double*>(p & ~uintptr_t(1));
+              if (p & 1u) store_granule_sys(row + t, x);
+              else store_granule(row + t, x);
+            } else {
+              store_granule(a.bnd + e * T + t, x);
+            }
           }
           // (the last step's Q, top width and side slope: route_last_kernel, from the saved states --
           // no rarely taken stores, and no pointers held across the tick loop for them)
@@ -888,6 +902,24 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int TT = (int)T + B.dmax;
   load_math_tables();
   load_xlist(a, B, xl);
+  // split basin: [nvirt] the virtuals' export rows (to the producer block's rank), then [ncout] the
+  // cut-outs' import rows (this rank's receive rows for edges from another rank's consumer)
+  uintptr_t* xtv = reinterpret_cast<uintptr_t*>(smem + a.xt_off);
+  uintptr_t* xtc = xtv + B.nvirt;
+  if (a.xt_off) {
+    for (int v = tid; v < B.nvirt; v += BS) {
+      const int64_t e = a.s.v_edge[B.virt0 + v];
+      const int xi = a.xid[e];
+      xtv[v] = xi >= 0 ? (reinterpret_cast<uintptr_t>(a.pxbwd[a.xprod[xi]] + (int64_t)xi * T * 2) | 1u)
+                       : reinterpret_cast<uintptr_t>(a.bwd_bnd + e * T * 2);
+    }
+    for (int c = tid; c < B.ncout; c += BS) {
+      const int64_t e = B.cout0 + c;
+      const int xi = a.xid[e];
+      xtc[c] = xi >= 0 ? (reinterpret_cast<uintptr_t>(a.xbwd + (int64_t)xi * T * 2) | 1u)
+                       : reinterpret_cast<uintptr_t>(a.bwd_bnd + e * T * 2);
+    }
+  }
   __syncthreads();
   unsigned long long prof_wait = 0;
   if (a.prof && tid == 0) prof_begin(a.prof, bid);
@@ -995,9 +1027,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         R A = R(0), Bv = R(0);
         if (t >= tmin && t < T) {
           double g[2];
-          const int xi = a.xid ? a.xid[B.cout0 + c] : -1;  // split basin: the consumer is another rank's block
-          if (xi >= 0) wait_granules<2, true>(a.xbwd + ((int64_t)xi * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
-          else wait_granules<2>(a.bwd_bnd + ((int64_t)(B.cout0 + c) * T + t) * 2, 0, 1, 0, 2, g, a.status, bid, force_to);
+          const uintptr_t p = a.xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
+          const double* row = reinterpret_cast<const double*>(p & ~uintptr_t(1)) + (int64_t)t * 2;
+          if (p & 1u) wait_granules<2, true>(row, 0, 1, 0, 2, g, a.status, bid, force_to);  // another rank's consumer
+          else wait_granules<2>(row, 0, 1, 0, 2, g, a.status, bid, force_to);
           A = R(g[0]);
           Bv = R(g[1]);
         }
@@ -1016,8 +1049,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int t = tau - v_off;
       if (t >= tmin && t < T) {
         const int dloc = v_dloc_of();
-        if (vxi >= 0) {  // split basin: the producer block is another rank's
-          double* dst = a.pxbwd[a.xprod[vxi]] + ((int64_t)vxi * T + t) * 2;
+        if (vxi >= 0) {  // split basin: the producer block is another rank's (row from the block's table)
+          double* dst = reinterpret_cast<double*>(xtv[tid] & ~uintptr_t(1)) + (int64_t)t * 2;
           store_granule_sys(dst, (double)sa[dloc]);
           store_granule_sys(dst + 1, (double)sb[dloc]);
         } else {
@@ -1502,14 +1535,24 @@ size_t route_smem_bytes(const Graph* g, bool backward) {
                          (size_t)g->max_xl, backward, sizeof(R));
 }
 
+// Split basin: after the layout, each block's granule rows (tagged pointers, bit 0 = another rank's
+// memory: system scope): forward, its cut-outs' export rows; backward, its virtuals' export rows then
+// its cut-outs' import rows -- resolved once per launch, no dependent global load per hand-off
+size_t split_table_bytes(const Graph* g, bool backward) {
+  if (g->split.nranks == 0) return 0;
+  return 8 * (size_t)(backward ? g->max_virt + g->max_cout : g->max_cout);
+}
+
 template <typename R, int KR>
 hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream_t stream) {
-  const size_t smem = route_smem_bytes<R>(g, backward);
+  const size_t base = route_smem_bytes<R>(g, backward);
+  const size_t smem = align16(base) + split_table_bytes(g, backward);
   a.slot_stride = route_slot_stride(g->max_slots);
   a.n_cut = g->n_cut;
   a.nblocks = (int32_t)g->blocks.size();
-  a.xl_off = (int32_t)(smem - (size_t)g->max_xl * 4);  // the lists close the LDS layout
+  a.xl_off = (int32_t)(base - (size_t)g->max_xl * 4);  // the lists close the base LDS layout
   a.own_off = a.xl_off - (int32_t)align16(4 * (size_t)std::max(g->max_virt, g->max_cout));
+  a.xt_off = g->split.nranks > 0 ? (int32_t)align16(base) : 0;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
     auto kern = a.gqs ? route_backward_kernel<R, KR, true> : route_backward_kernel<R, KR, false>;
@@ -1556,7 +1599,7 @@ hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipSt
 template <typename R>
 int max_resident_blocks(const Graph* g, bool backward) {
   int nb = 0;
-  const size_t smem = route_smem_bytes<R>(g, backward);
+  const size_t smem = align16(route_smem_bytes<R>(g, backward)) + split_table_bytes(g, backward);
   const void* f = nullptr;
   switch (g->kr) {
     case 1: f = backward ? (const void*)route_backward_kernel<R, 1, false> : (const void*)route_forward_kernel<R, 1, 0>; break;

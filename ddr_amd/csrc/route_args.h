@@ -64,6 +64,7 @@ struct RouteArgs {
   double* xbwd;
   double* pxfwd[kMaxSplitRanks];
   double* pxbwd[kMaxSplitRanks];
+  int32_t xt_off;  // split: byte offset of the block's granule row table in the dynamic LDS (0: none)
   double c[8];  // dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub
   float cf[8];  // the same rounded to fp32 (kernel constants of the fp32 build)
   double ln_dlb;  // ln of the fp32-rounded depth lower bound (fp32 pow derivation, physics.h)

@@ -24,18 +24,92 @@ from . import _lib
 from .partition import basin_labels, extract_basins, shard_basins
 
 
-def plan_block_ranks(nloc, k: int) -> np.ndarray:
-    """Rank of each logical block: k contiguous ranges of the ticket order with equal reach counts."""
+def plan_block_ranks(nloc, k: int, prod=None, cons=None, tol: float = 0.05, sweeps: int = 8) -> np.ndarray:
+    """Rank of each logical block: k contiguous ranges with equal reach counts -- of the ticket order,
+    or (given the cut edges' producer / consumer blocks) of a depth-first order of the block graph from
+    the outlet side when that crosses fewer edges -- then greedy moves of single blocks to the rank most
+    of their cut edges lead to, while every rank stays within ``tol`` of the mean load: fewer
+    cross-rank edges (each a system-scope hand-off over xGMI) for the same balance.  Deterministic,
+    so every rank of a split computes the same plan.  Any assignment is deadlock-free: each rank takes
+    its blocks in ticket (topological) order."""
     nloc = np.asarray(nloc, dtype=np.int64)
     if k < 1 or len(nloc) < k:
         raise ValueError("need at least one block per rank")
-    mid = np.cumsum(nloc) - nloc / 2.0
-    r = np.minimum((mid * k / max(float(nloc.sum()), 1.0)).astype(np.int64), k - 1)
-    # every rank gets at least one block (tiny graphs)
-    for i in range(k):
-        if not np.any(r == i):
-            r[min(i, len(r) - 1)] = i
-    return np.maximum.accumulate(r).astype(np.int32)
+
+    def ranges(order):  # k contiguous ranges of `order` with equal reach counts
+        w = nloc[order]
+        mid = np.cumsum(w) - w / 2.0
+        rr = np.minimum((mid * k / max(float(nloc.sum()), 1.0)).astype(np.int64), k - 1)
+        for i in range(k):  # every rank gets at least one block (tiny graphs)
+            if not np.any(rr == i):
+                rr[min(i, len(rr) - 1)] = i
+        out = np.empty(len(order), dtype=np.int64)
+        out[order] = np.maximum.accumulate(rr)
+        return out
+
+    nb = len(nloc)
+    r = ranges(np.arange(nb))
+    if prod is None or cons is None or k == 1 or len(prod) == 0:
+        return r.astype(np.int32)
+    prod = np.asarray(prod, dtype=np.int64)
+    cons = np.asarray(cons, dtype=np.int64)
+    nbr = [[] for _ in range(nb)]
+    for a, b in zip(prod.tolist(), cons.tolist()):
+        nbr[a].append(b)
+        nbr[b].append(a)
+    # depth-first order of the block graph from the outlet side (the last tickets): contiguous ranges
+    # of it are unions of whole upstream subtrees, crossed by few edges
+    seen = np.zeros(nb, dtype=bool)
+    order = []
+    for root in range(nb - 1, -1, -1):
+        if seen[root]:
+            continue
+        stack = [root]
+        seen[root] = True
+        while stack:
+            b = stack.pop()
+            order.append(b)
+            for c in sorted(nbr[b], reverse=True):
+                if not seen[c]:
+                    seen[c] = True
+                    stack.append(c)
+    rd = ranges(np.asarray(order, dtype=np.int64))
+    if np.count_nonzero(rd[prod] != rd[cons]) < np.count_nonzero(r[prod] != r[cons]):
+        r = rd
+    load = np.bincount(r, weights=nloc, minlength=k).astype(np.float64)
+    mean = float(nloc.sum()) / k
+    lo, hi = mean * (1.0 - tol), mean * (1.0 + tol)
+    for _ in range(sweeps):
+        moved = 0
+        for b in range(nb):
+            if not nbr[b]:
+                continue
+            cnt = np.bincount(r[nbr[b]], minlength=k)
+            cur = r[b]
+            best = int(np.argmax(cnt))
+            if best == cur or cnt[best] <= cnt[cur]:
+                continue
+            if load[best] + nloc[b] > hi or load[cur] - nloc[b] < lo or np.count_nonzero(r == cur) == 1:
+                continue
+            r[b] = best
+            load[best] += nloc[b]
+            load[cur] -= nloc[b]
+            moved += 1
+        if moved == 0:
+            break
+    return r.astype(np.int32)
+
+
+def block_edges(graph):
+    """(nloc per logical block, producer block and consumer block of every cut edge) of a RiverGraph."""
+    lib = _lib.load()
+    info = graph.info
+    nloc = np.zeros(info.n_blocks, dtype=np.int32)
+    _lib.check(lib.ddr_graph_blocks(graph.handle, nloc.ctypes.data, len(nloc)))
+    prod = np.empty(max(info.n_cut, 1), dtype=np.int32)
+    cons = np.empty(max(info.n_cut, 1), dtype=np.int32)
+    _lib.check(lib.ddr_graph_cut_blocks(graph.handle, prod.ctypes.data, cons.ctypes.data, int(info.n_cut)))
+    return nloc, prod[:info.n_cut], cons[:info.n_cut]
 
 
 def plan_ranks(n: int, rows, cols, world: int, factor: float = 2.0, force: bool = False):
@@ -95,10 +169,7 @@ class SplitBasin:
         self.block_rank = np.ascontiguousarray(block_rank, dtype=np.int32)
         if len(self.block_rank) != info.n_blocks:
             raise ValueError("block_rank needs one entry per logical block")
-        prod = np.empty(max(info.n_cut, 1), dtype=np.int32)
-        cons = np.empty(max(info.n_cut, 1), dtype=np.int32)
-        _lib.check(lib.ddr_graph_cut_blocks(graph.handle, prod.ctypes.data, cons.ctypes.data, int(info.n_cut)))
-        prod, cons = prod[:info.n_cut], cons[:info.n_cut]
+        _, prod, cons = block_edges(graph)
         self.n_x = int(np.count_nonzero(self.block_rank[prod] != self.block_rank[cons]))
         nb = C.c_int64()
         _lib.check(lib.ddr_xmem_bytes(self.n_x, int(t_cap), C.byref(nb)))

@@ -50,16 +50,15 @@ def main():
     from ddr_amd import _lib
     from ddr_amd.graph import RiverGraph
     from ddr_amd.ops import check_status
-    from ddr_amd.split import SplitBasin, plan_block_ranks
+    from ddr_amd.split import SplitBasin, block_edges, plan_block_ranks
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     net, at, u, qp, W = case()
     g = RiverGraph(net.n, net.rows, net.cols, **GRAPH_KW)
-    nloc = np.zeros(g.info.n_blocks, dtype=np.int32)
-    _lib.check(_lib.load().ddr_graph_blocks(g.handle, nloc.ctypes.data, len(nloc)))
-    br = plan_block_ranks(nloc, world)
+    nloc, prod, cons = block_edges(g)
+    br = plan_block_ranks(nloc, world, prod, cons)
 
     def exchange(obj):
         res = [None] * world

@@ -42,3 +42,26 @@ def test_rank_plan_splits_only_a_dominant_basin():
     assert max(sizes) < np.count_nonzero(lab == big) / 2  # the others are balanced below the basin's share
     forced = plan_ranks(net.n, net.rows, net.cols, 2, force=True)
     assert all(s is not None for _, s in forced)
+
+
+def test_block_rank_refinement_cuts_fewer_edges_within_balance():
+    # a chain of 4 trees of blocks: each tree's blocks interleaved in ticket order (as piece heights do)
+    rng = np.random.default_rng(3)
+    nb, k = 400, 4
+    tree = np.arange(nb) % 4
+    nloc = rng.integers(200, 300, nb)
+    prod, cons = [], []
+    for t in range(4):
+        ids = np.nonzero(tree == t)[0]
+        for i in range(1, len(ids)):  # each block feeds the next block of its tree
+            prod.append(ids[i - 1])
+            cons.append(ids[i])
+    prod, cons = np.array(prod), np.array(cons)
+    r0 = plan_block_ranks(nloc, k)
+    r1 = plan_block_ranks(nloc, k, prod, cons, tol=0.05)
+    x0 = np.count_nonzero(r0[prod] != r0[cons])
+    x1 = np.count_nonzero(r1[prod] != r1[cons])
+    assert x1 < x0
+    load = np.bincount(r1, weights=nloc, minlength=k)
+    assert load.max() <= nloc.sum() / k * 1.05 + 1 and load.min() >= nloc.sum() / k * 0.95 - 1
+    assert np.array_equal(r1, plan_block_ranks(nloc, k, prod, cons, tol=0.05))  # deterministic
