@@ -331,6 +331,14 @@ def main():
     n_loc, rows, cols, ids = shard_network(net.n, net.rows, net.cols, rank, world) if world > 1 else (
         net.n, net.rows, net.cols, np.arange(net.n))
     g, split = None, None
+    if alone and os.environ.get("DDR_BENCH_SPLIT_PLAN") == "1":
+        # prediction runs: a rank outside the split group, with the shard the split plan gives it
+        from ddr_amd.split import plan_ranks, sub_network
+
+        ids_r, sp = plan_ranks(net.n, net.rows, net.cols, world)[rank]
+        if sp is not None:
+            raise SystemExit("a split-group rank cannot run alone (its blocks wait for its peers)")
+        n_loc, rows, cols, ids = sub_network(net.n, net.rows, net.cols, ids_r)
     if args.workload == "c5" and world > 1 and not alone and os.environ.get("DDR_SPLIT_BASIN", "1") != "0":
         plan = setup_split(args, net, rank, world, dist, dev, T)
         if plan is not None:

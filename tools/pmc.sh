@@ -21,5 +21,5 @@ run p5 GRBM_GUI_ACTIVE GRBM_COUNT TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum &&
 rc=$?
 python3 $R/tools/pmc_report.py $OUT > $OUT/report.txt 2>&1
 cat $OUT/report.txt
-find $OUT -name "*.db" -delete
+[ "${KEEP_DB:-0}" = 1 ] || find $OUT -name "*.db" -delete
 exit $rc

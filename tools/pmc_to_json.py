@@ -22,10 +22,19 @@ vals = defaultdict(dict)
 dbs = sorted(glob.glob(f"{root}/p*/run_results.db"))
 for db in dbs:
     c = sqlite3.connect(db)
-    q = ("select kernel_name, counter_name, sum(value), count(distinct dispatch_id) from counters_collection "
-         "group by kernel_name, counter_name")
-    for k, cn, v, nd in c.execute(q):
-        vals[k][cn] = v / max(nd, 1)
+    q = ("select kernel_name, dispatch_id, counter_name, sum(value) from counters_collection "
+         "group by kernel_name, dispatch_id, counter_name")
+    per = defaultdict(lambda: defaultdict(dict))
+    for k, disp, cn, v in c.execute(q):
+        per[k][disp][cn] = v
+    # a kernel launched with different windows in one step (C4: the 365-day accumulation and the
+    # water-year forward are both route_forward_kernel): average the dispatches of the big launch only
+    for k, ds in per.items():
+        size = {d: sum(cv.values()) for d, cv in ds.items()}
+        top = max(size.values())
+        keep = [d for d in ds if size[d] >= 0.25 * top]
+        for cn in {cn for d in keep for cn in ds[d]}:
+            vals[k][cn] = sum(ds[d].get(cn, 0.0) for d in keep) / len(keep)
 if not dbs:  # the databases were pruned: read tools/pmc_report.py's summary instead
     cur = None
     for line in Path(root, "report.txt").read_text().splitlines():
@@ -57,7 +66,9 @@ for k, d in vals.items():
     kernels[name] = e
 out = {"workload": workload, "build": build, "T": int(T), "reaches": int(reaches), "source": source,
        "kernels": kernels}
-dst = Path(__file__).resolve().parents[1] / "profiles" / "counters" / f"{workload}.json"
+import os  # noqa: E402
+
+dst = Path(os.environ.get("PMC_JSON_DIR") or Path(__file__).resolve().parents[1] / "profiles" / "counters") / f"{workload}.json"
 dst.parent.mkdir(parents=True, exist_ok=True)
 dst.write_text(json.dumps(out, indent=1))
 print(dst, {k: {kk: vv for kk, vv in v.items() if kk != "counters"} for k, v in kernels.items()})
