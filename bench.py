@@ -616,7 +616,7 @@ def time_training_stream(args, dev):
         un = model(d["feats"])
         n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
         daily, _, _, _ = route(g, d["qprime"], n, q, p, d["length"], d["slope"], d["xs"], gauges=d["gz"],
-                               daily=window, consts=consts, steps=T, qprime_hours=24)
+                               daily=window, consts=consts, steps=T, qprime_hours=24, math=args.math)
         loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])
         loss.backward()
         allreduce_gradients(list(model.parameters()))
@@ -643,6 +643,10 @@ def time_training_stream(args, dev):
             # wall time per step not inside a training step's own GPU span: the next batches' device
             # builds (queued between steps on the training stream) and any device idle time
             "between_steps_ms": timed / K * 1e3 - gpu,
+            "stream_over_gpu_step": timed / K * 1e3 / gpu,
+            "graph_wait_note": "host time in next(prefetcher): the host runs ahead of the device and waits there "
+                               "for its queue (device builds are stream-ordered between training steps); the "
+                               "device-side cost of the builds is between_steps_ms",
             "ns_per_reach_step_gpu": float(np.mean([b["step_gpu_ms"] * 1e6 / (b["reaches"] * (T - 1)) for b in per])),
             "batches": per,
             "note": (f"new adjacency + graph build per step ({BUILDERS[args.stream_builder]}"

@@ -244,6 +244,15 @@ def test_c2_full_water_year_matches_oracle(cuda):
     ff = FullForest(net, 2, cuda)
     ref = ff.oracle(np.arange(net.n), grads=False)
     assert maxrel(ff.out["runoff"].cpu().numpy(), ref["runoff"]) <= 1e-6
+    # the benched arithmetic (faithful: IEEE divisions, fp32 pow within 1 ulp) and the fast one, over the
+    # whole water year against the same fp32 oracle (correctly rounded pow): north star 1e-4 max-rel
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    for math, tol in (("faithful", 1e-5), ("fast", 1e-4)):
+        with torch.no_grad():
+            runoff, _, _, _ = route(ff.graph, ff.qprime, tt(ff.n), tt(ff.q), tt(ff.p), tt(ff.length), tt(ff.slope),
+                                    tt(ff.x), consts=RouteConsts(), save=False, math=math)
+        err = maxrel(runoff.cpu().numpy(), ref["runoff"])
+        assert err <= tol, (math, err)
 
 
 # ---- C3: the training batch of 256 gauged subnetworks ------------------------------------------
