@@ -41,6 +41,7 @@ DDR_FWD_FAITHFUL_MATH = 32
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 DDR_DEBUG_NO_STEADY = 2
+DDR_DEBUG_NO_STORER = 4
 
 
 class BuildOpts(C.Structure):

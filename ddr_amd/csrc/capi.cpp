@@ -46,7 +46,8 @@ struct KernelTiming {
 unsigned long long* g_prof[2] = {nullptr, nullptr};
 int32_t g_debug = [] {  // ddr_set_debug_flags (DDR_NO_STEADY=1: the general tick path only, for A/B)
   const char* e = std::getenv("DDR_NO_STEADY");
-  return (e && e[0] == '1') ? kFlagNoSteady : 0;
+  const char* f = std::getenv("DDR_NO_STORER");
+  return ((e && e[0] == '1') ? kFlagNoSteady : 0) | ((f && f[0] == '1') ? kFlagNoStorer : 0);
 }();
 
 // Hand-off failures surface without a host sync on the hot path: after every routing launch the
@@ -864,7 +865,8 @@ ddr_status ddr_status_check(int32_t wait) {
 }
 
 ddr_status ddr_set_debug_flags(int32_t flags) {
-  g_debug = ((flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0) | ((flags & DDR_DEBUG_NO_STEADY) ? kFlagNoSteady : 0);
+  g_debug = ((flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0) | ((flags & DDR_DEBUG_NO_STEADY) ? kFlagNoSteady : 0) |
+            ((flags & DDR_DEBUG_NO_STORER) ? kFlagNoStorer : 0);
   return DDR_OK;
 }
 

@@ -288,5 +288,6 @@ constexpr int kStatusTicketBwd = 3;
 // RouteArgs.flags bits beyond the public DDR_FWD_* flags
 constexpr int32_t kFlagForceTimeout = 1 << 16;  // debug: every inter-workgroup wait times out
 constexpr int32_t kFlagNoSteady = 1 << 17;      // debug / A/B: every tick through the general path
+constexpr int32_t kFlagNoStorer = 1 << 18;      // debug / A/B: light blocks store from their compute waves
 
 }  // namespace ddr

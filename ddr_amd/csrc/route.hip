@@ -421,6 +421,21 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const bool emit = runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
   // rows 16-B aligned: vector stores (per-step 4-B stores measured 1.6x slower for the whole kernel)
   const bool emit4 = (T & 3) == 0;
+  // Storer waves (one reach per thread, blocks of at most half a workgroup): the idle upper half of the
+  // workgroup stores each reach's published x (x_save row, runoff) during the next tick, so a compute
+  // wave's top-of-tick wait covers only its q' prefetch -- not the acknowledgement of its stores, which
+  // is on a light block's critical path (up to 12 % of a C2 tick, profiles/r03/ab_r03.txt item 5)
+#ifndef DDR_FWD_STORER
+#define DDR_FWD_STORER 1
+#endif
+  const bool storer_mode = KR == 1 && DDR_FWD_STORER && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2;
+  const bool storer_wave = storer_mode && wbase >= BS / 2;
+  const int sr = tid - BS / 2;  // a storer thread's reach
+  int sref = 0, soff = 0;
+  if (storer_wave && sr < B.nloc) {
+    sref = a.s.ref[B.pos0 + sr];
+    soff = a.s.off[B.pos0 + sr];
+  }
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -492,12 +507,41 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // sc: std::integral_constant<bool, kSt>.  Steady ticks (tau in [dmax + 1, T - 1]) are those at which
   // every reach of the block runs a step t in [1, T - 1]: no activity tests, no idle-slice ballot, no
   // hot start or carried-state case -- the same operations on the same values as the general tick
+  // storer threads: the stores of the x their reach published at tick `taup` (read from its slot before
+  // the next publish overwrites it); the same values and rounding as the compute waves' stores
+  auto store_pass = [&](int taup) {
+    if (sr >= B.nloc) return;
+    const int t = taup - opq(soff);
+    if (t < 0 || t >= T) return;
+    const R xr = R(sx[sr]);
+    static_cast<R*>(a.x_save)[xs_base + (int64_t)taup * B.nloc + sr] = xr;
+    if (emit) {
+      ob0[0] = ob1[0];
+      ob1[0] = ob2[0];
+      ob2[0] = ob3[0];
+      ob3[0] = rmax_nan(xr, cs.qlb);
+      R* orow = runoff + (int64_t)opq(sref) * T;
+      if (!emit4) orow[t] = ob3[0];
+      else if ((t & 3) == 3) store4(orow + (t - 3), ob0[0], ob1[0], ob2[0], ob3[0]);
+    }
+  };
+
   auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR], auto sc) {
     constexpr bool kSt = decltype(sc)::value;
+    if constexpr (KR == 1) {
+      // a storer wave issues no q' loads: it never waits for its stores (its import owners wait only for
+      // their granules, requested before this tick's stores -- store_pass runs after the import)
+      if (!storer_wave) {
 #if DDR_FWD_TOPWAIT
-    // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
-    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
+      }
+    } else {
+#if DDR_FWD_TOPWAIT
+      // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
+      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#endif
+    }
     phz.mark(0);  // the previous tick's loads and stores
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
@@ -544,6 +588,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     phz.mark(1);  // import
+    if constexpr (KR == 1) {
+      if (storer_wave && tau > 0) store_pass(tau - 1);
+    }
     prefetch(tau + 1, qnext, tq, sc);
     R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
@@ -637,8 +684,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #ifndef DDR_EXP_NO_FWD_STORES
 #define DDR_EXP_NO_FWD_STORES 0  // timing experiment only: no x_save / runoff stores (wrong results)
 #endif
-          if (!DDR_EXP_NO_FWD_STORES) xrow[r] = xr;  // the routing state for the adjoint
-          if (emit && !DDR_EXP_NO_FWD_STORES) {
+          const bool own_st = !DDR_EXP_NO_FWD_STORES && !storer_mode;  // (storer mode: the upper waves store)
+          if (own_st) xrow[r] = xr;  // the routing state for the adjoint
+          if (emit && own_st) {
             // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
             ob0[k] = ob1[k];
             ob1[k] = ob2[k];
@@ -729,6 +777,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
 #endif
+  if constexpr (KR == 1) {
+    if (storer_wave) store_pass(TT - 1);  // the last tick's publish (its barrier has passed)
+  }
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
   phz.flush(a.prof, a.nblocks, bid);
 }

@@ -15,9 +15,9 @@ from ddr_amd.ops import GaugeMap, route
 pytestmark = pytest.mark.gpu
 
 
-def _run(case, dev, g, math, q0=None, gauges=None, no_steady=False):
+def _run(case, dev, g, math, q0=None, gauges=None, no_steady=False, flags=None):
     lib = _lib.load()
-    _lib.check(lib.ddr_set_debug_flags(_lib.DDR_DEBUG_NO_STEADY if no_steady else 0))
+    _lib.check(lib.ddr_set_debug_flags(flags if flags is not None else (_lib.DDR_DEBUG_NO_STEADY if no_steady else 0)))
     try:
         tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev, torch.float32)  # noqa: E731
         u = {k: tt(case.u[k]).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial")}
@@ -64,3 +64,19 @@ def test_steady_path_gauge_mode(cuda):
     b = _run(case, cuda, g, "faithful", gauges=gz, no_steady=True)
     for k in a:
         assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("T", [300, 302], ids=["rows16B", "ragged"])
+def test_storer_waves_are_bitwise_the_compute_wave_stores(cuda, T):
+    """Light blocks (<= 512 reaches, one per thread) store x_save / runoff from their idle upper waves;
+    outputs and gradients equal the compute-wave stores bit for bit (T % 4 != 0: per-step runoff stores)."""
+    net = synthetic.forest(synthetic.loguniform_sizes(12, 50, 3000, 11), seed=11)
+    case = synthetic_case(net, T, 11)
+    g = RiverGraph(net.n, net.rows, net.cols, max_block_reaches=256, target_blocks=1 << 20)
+    assert g.info.reaches_per_thread == 1
+    q0 = np.random.default_rng(12).uniform(0.1, 5.0, net.n).astype(np.float32)
+    for kw in ({}, {"q0": q0}):
+        a = _run(case, cuda, g, "faithful", flags=0, **kw)
+        b = _run(case, cuda, g, "faithful", flags=_lib.DDR_DEBUG_NO_STORER, **kw)
+        for k in a:
+            assert np.array_equal(a[k], b[k], equal_nan=True), k
