@@ -123,6 +123,7 @@ _SIGS = {
     "ddr_graph_blocks": (C.c_int, [_P, _P, _I64]),
     "ddr_graph_cut_blocks": (C.c_int, [_P, _P, _P, _I64]),
     "ddr_graph_set_split": (C.c_int, [_P, _I32, _I32, _P, _P, _P, _I64, C.POINTER(C.c_int64)]),
+    "ddr_graph_clear_split": (C.c_int, [_P]),
     "ddr_status_check": (C.c_int, [_I32]),
     "ddr_set_debug_flags": (C.c_int, [_I32]),
     "ddr_tri_solve": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _P]),

@@ -687,6 +687,15 @@ ddr_status ddr_graph_set_split(ddr_graph* gh, int32_t rank, int32_t nranks, cons
   })
 }
 
+ddr_status ddr_graph_clear_split(ddr_graph* gh) {
+  if (!gh) return fail(DDR_ERR_ARG, "null graph");
+  Graph* g = reinterpret_cast<Graph*>(gh);
+  // the device arrays stay with the graph (freed at destroy); the receive memory is the caller's
+  const SplitState none;
+  g->split = none;
+  return DDR_OK;
+}
+
 ddr_status ddr_graph_get_info(const ddr_graph* gh, ddr_graph_info* info) {
   if (!gh || !info) return fail(DDR_ERR_ARG, "null argument");
   const Graph* g = reinterpret_cast<const Graph*>(gh);

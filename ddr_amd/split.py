@@ -185,26 +185,32 @@ class SplitBasin:
         except Exception as e:  # noqa: BLE001  (still take part in the exchange: the peers wait for it)
             err = e
         handles = exchange(None if err else bytes(handle))
-        if err is not None:
-            raise err
-        if len(handles) != k:
-            raise ValueError("exchange must return one handle per rank of the group")
-        if any(h is None for h in handles):
-            raise RuntimeError("split basin: a peer could not allocate its receive memory")
-        for r, h in enumerate(handles):
-            if r == index:
-                self.peers.append(self.local)
-                continue
-            p = C.c_void_p()
-            _lib.check(lib.ddr_xmem_open((C.c_ubyte * 64).from_buffer_copy(h), C.byref(p)))
-            self.peers.append(p.value)
-            self._opened.append(p.value)
-        arr = (C.c_void_p * k)(*self.peers)
-        n_x = C.c_int64()
-        _lib.check(lib.ddr_graph_set_split(graph.handle, index, k, self.block_rank.ctypes.data, self.local, arr,
-                                           int(t_cap), C.byref(n_x)))
-        if n_x.value != self.n_x:
-            raise RuntimeError("cross-rank cut edges disagree between the host plan and the library")
+        self._attached = False
+        try:
+            if err is not None:
+                raise err
+            if len(handles) != k:
+                raise ValueError("exchange must return one handle per rank of the group")
+            if any(h is None for h in handles):
+                raise RuntimeError("split basin: a peer could not allocate its receive memory")
+            for r, h in enumerate(handles):
+                if r == index:
+                    self.peers.append(self.local)
+                    continue
+                p = C.c_void_p()
+                _lib.check(lib.ddr_xmem_open((C.c_ubyte * 64).from_buffer_copy(h), C.byref(p)))
+                self.peers.append(p.value)
+                self._opened.append(p.value)
+            arr = (C.c_void_p * k)(*self.peers)
+            n_x = C.c_int64()
+            _lib.check(lib.ddr_graph_set_split(graph.handle, index, k, self.block_rank.ctypes.data, self.local, arr,
+                                               int(t_cap), C.byref(n_x)))
+            self._attached = True
+            if n_x.value != self.n_x:
+                raise RuntimeError("cross-rank cut edges disagree between the host plan and the library")
+        except Exception:
+            self.close()  # neither opened handles nor the receive memory leak
+            raise
         # the reaches this rank routes (their outputs and gradients are this rank's)
         blk = graph.structure()["block"] if hasattr(graph, "structure") else None
         self.owned_reaches = None if blk is None else np.nonzero(self.block_rank[blk] == index)[0]
@@ -215,6 +221,9 @@ class SplitBasin:
 
         lib = _lib.load()
         torch.cuda.synchronize()
+        if getattr(self, "_attached", False) and self.graph.handle is not None and self.graph.handle.value:
+            _lib.check(lib.ddr_graph_clear_split(self.graph.handle))  # no later launch touches freed memory
+        self._attached = False
         for p in self._opened:
             _lib.check(lib.ddr_xmem_close(p, 1))
         self._opened = []

@@ -358,6 +358,9 @@ ddr_status ddr_graph_cut_blocks(const ddr_graph* g, int32_t* prod, int32_t* cons
  * (returned in *n_x) */
 ddr_status ddr_graph_set_split(ddr_graph* g, int32_t rank, int32_t nranks, const int32_t* block_rank, void* local,
                                void* const* peers, int64_t t_cap, int64_t* n_x);
+/* detach the split (before its receive memory is released): later launches run every block again.
+ * One stream per split graph: its launch epochs are counted per graph. */
+ddr_status ddr_graph_clear_split(ddr_graph* g);
 
 /* Debug knobs.  DDR_DEBUG_FORCE_TIMEOUT: every inter-workgroup wait of the following launches
  * times out (tests the failure path).  DDR_DEBUG_NO_STEADY: the routing kernels run every tick
