@@ -363,7 +363,7 @@ def main():
     qprime = synthetic.lateral_inflow_torch(net.n, -(-T // qp_hours), seed=11, device=dev, ids=ids)
     consts = RouteConsts()
     lib = _lib.load()
-    lib_hash = lib.ddr_version().decode().split()[-1]
+    lib_hash = lib.ddr_version().decode().split()[-1]  # the routing kernels' hash (key of the counter files)
     # algorithmic bytes per reach-step, SURVEY §8(d): forward q' read + x_save write + runoff write; backward
     # dL/drunoff read + x_save read + q' read; gauge mode (C3) has no per-reach runoff / dL/drunoff (G x T
     # only).  These are the roofline's figures.  The fp32 adjoint itself never reads q' (the c4 term of the

@@ -912,6 +912,12 @@ const char* ddr_last_error(void) { return ddr::last_error_cstr(); }
 #ifndef DDR_SOURCE_HASH
 #define DDR_SOURCE_HASH "unknown"
 #endif
-const char* ddr_version(void) { return "ddr_mc 0.2.0 (gfx950) src " DDR_SOURCE_HASH; }
+// src: every library source; kern: the routing kernels' sources only (route.hip and the headers it
+// includes) -- the key of the PMC counter files under profiles/counters (bench.py), which describe the
+// kernels and stay valid across host-side changes.  The kernel hash is the last word.
+#ifndef DDR_KERNEL_HASH
+#define DDR_KERNEL_HASH "unknown"
+#endif
+const char* ddr_version(void) { return "ddr_mc 0.2.0 (gfx950) src " DDR_SOURCE_HASH " kern " DDR_KERNEL_HASH; }
 
 }  // extern "C"
