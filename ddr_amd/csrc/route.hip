@@ -431,10 +431,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const bool storer_mode = KR == 1 && DDR_FWD_STORER && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2;
   const bool storer_wave = storer_mode && wbase >= BS / 2;
   const int sr = tid - BS / 2;  // a storer thread's reach
-  int sref = 0, soff = 0;
+  // storer-side granule exports too (DDR_FWD_STORER_GRANULES): a cut reach's x reaches its consumer one
+  // tick later (pipeline latency of that hand-off only), and no compute wave waits for a store at all
+#ifndef DDR_FWD_STORER_GRANULES
+#define DDR_FWD_STORER_GRANULES 1
+#endif
+  int sref = 0, soff = 0;  // soff: tick offset | 1 + cut rank << 16, as off[]
   if (storer_wave && sr < B.nloc) {
     sref = a.s.ref[B.pos0 + sr];
-    soff = a.s.off[B.pos0 + sr];
+    const int e = a.s.cut[B.pos0 + sr];
+    soff = a.s.off[B.pos0 + sr] | (e >= 0 ? (e - B.cout0 + 1) << 16 : 0);
   }
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
@@ -511,9 +517,22 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // the next publish overwrites it); the same values and rounding as the compute waves' stores
   auto store_pass = [&](int taup) {
     if (sr >= B.nloc) return;
-    const int t = taup - opq(soff);
+    const int so = opq(soff);
+    const int t = taup - (so & 0xFFFF);
     if (t < 0 || t >= T) return;
-    const R xr = R(sx[sr]);
+    const double xd = sx[sr];
+    const R xr = R(xd);
+    if (DDR_FWD_STORER_GRANULES && B.ncout > 0 && (so >> 16)) {
+      const int64_t e = B.cout0 + (so >> 16) - 1;
+      if (a.xt_off) {
+        const uintptr_t p = xt[(so >> 16) - 1];
+        double* row = reinterpret_cast<double*>(p & ~uintptr_t(1));
+        if (p & 1u) store_granule_sys(row + t, xd);
+        else store_granule(row + t, xd);
+      } else {
+        store_granule(a.bnd + e * T + t, xd);
+      }
+    }
     static_cast<R*>(a.x_save)[xs_base + (int64_t)taup * B.nloc + sr] = xr;
     if (emit) {
       ob0[0] = ob1[0];
@@ -696,7 +715,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
-          if (B.ncout > 0 && (off[k] >> 16)) {
+          if (B.ncout > 0 && (off[k] >> 16) && !(DDR_FWD_STORER_GRANULES && storer_mode)) {
             const int64_t e = B.cout0 + (off[k] >> 16) - 1;
             if (a.xt_off) {  // split basin: the row from the block's table (another rank's: system scope)
               const uintptr_t p = xt[(off[k] >> 16) - 1];
