@@ -233,6 +233,9 @@ def setup_split(args, net, rank, world, dist, dev, T):
         try:  # hand-shake: a short forward on the split graph, every cross-rank edge exercised
             from ddr_amd.ops import check_status
 
+            if os.environ.get("DDR_SPLIT_FAIL_RANK") == str(rank):  # rehearsal of the fallback path
+                raise RuntimeError("simulated hand-shake failure (DDR_SPLIT_FAIL_RANK)")
+
             Th = min(T, 48)
             z = torch.full((n_loc,), 0.5, device=dev)
             route(g, torch.full((Th, n_loc), 0.1, device=dev), z * 0.1, z, z * 10, z * 1000 + 1000, z * 0.01, z * 0.5,

@@ -75,9 +75,14 @@ struct PendingStatus {
       char id[96];
       snprintf(id, sizeof(id), " (graph %p, stream %p, routing launch #%llu of this process)", graph[k],
                (void*)stream[k], seq[k]);
-      msg = std::to_string(w[0]) + " inter-workgroup hand-offs of a " + what[k] + " launch" + id +
-            " timed out (first logical block " + std::to_string((int)w[1] - 1) +
-            "); its outputs hold NaN. Reported by the next library call: call ddr_status_check(1) at the "
+      // word 1: first failing logical block + 1, or 0x40000000 + rank for a split basin's peer that never
+      // arrived at the launch's epoch hand-shake (route.hip: split_barrier_kernel)
+      const std::string where = w[1] >= 0x40000000u
+                                    ? "split-basin hand-shake: rank " + std::to_string((int)(w[1] - 0x40000000u)) +
+                                          " never arrived"
+                                    : "first logical block " + std::to_string((int)w[1] - 1);
+      msg = std::to_string(w[0]) + " inter-workgroup hand-offs of a " + what[k] + " launch" + id + " timed out (" +
+            where + "); its outputs hold NaN. Reported by the next library call: call ddr_status_check(1) at the "
             "end of a run so that a timeout in the last launch is not missed";
     }
     (void)hipEventDestroy(ev[k]);
