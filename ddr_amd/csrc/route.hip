@@ -137,6 +137,54 @@ __device__ __forceinline__ void wait_granules(const double* row, int64_t t0, int
   for (int s = 0; s < C; ++s) out[s] = __longlong_as_double(v[s]);
 }
 
+// Split form of wait_granules for imports requested a chunk ahead: issue_granules requests the granules
+// (no wait: they land while the block runs on), poll_granules waits for the still-unpublished ones with the
+// same bounds and failure handling as wait_granules.
+template <int C, bool Sys>
+__device__ __forceinline__ void issue_granules(const double* row, int64_t t0, int64_t lo, int64_t hi,
+                                               unsigned long long (&v)[C]) {
+#pragma unroll
+  for (int s = 0; s < C; ++s) {
+    const int64_t t = t0 + s;
+    v[s] = (t >= lo && t < hi) ? (Sys ? load_granule_sys(row + t) : load_granule(row + t)) : 0ull;
+  }
+}
+template <int C, bool Sys>
+__device__ __forceinline__ void poll_granules(const double* row, int64_t t0, int64_t lo, int64_t hi,
+                                              unsigned long long (&v)[C], double (&out)[C], unsigned* status, int bid,
+                                              bool force_timeout) {
+  auto ld = [](const double* p) { return Sys ? load_granule_sys(p) : load_granule(p); };
+  unsigned pend = 0;
+#pragma unroll
+  for (int s = 0; s < C; ++s) pend |= (v[s] == kSentinel ? 1u : 0u) << s;
+  unsigned spins = 0;
+  while (pend != 0u || force_timeout) {
+    ++spins;
+    const bool failed = (spins & 1023u) == 0u &&
+                        __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    if (force_timeout || failed || spins > (1u << 24)) {
+      atomicAdd(status, 1u);
+      atomicCAS(status + 1, 0u, (unsigned)bid + 1u);
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int64_t t = t0 + s;
+        const bool nan = ((pend >> s) & 1u) || (force_timeout && t >= lo && t < hi);
+        v[s] = nan ? 0x7FF8000000000000ull : v[s];
+      }
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const unsigned long long w = ((pend >> s) & 1u) ? ld(row + (t0 + s)) : v[s];
+      v[s] = w;
+      pend &= ~((w != kSentinel ? 1u : 0u) << s);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < C; ++s) out[s] = __longlong_as_double(v[s]);
+}
+
 // Logical block of this workgroup: the next ticket of the launch (forward: blocks in piece-height
 // order, backward: the reverse).  A workgroup waits only on blocks of lower logical index, whose
 // tickets were taken by workgroups already running or finished: no co-residency assumption.
@@ -428,6 +476,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #ifndef DDR_FWD_STORER
 #define DDR_FWD_STORER 1
 #endif
+  // imports requested a chunk ahead (KR <= 2: registers for the chunk's raw granules)
+#ifndef DDR_FWD_PREF_IMPORT
+#define DDR_FWD_PREF_IMPORT 1
+#endif
+  constexpr bool kPrefImport = DDR_FWD_PREF_IMPORT && KR <= 2;
+  unsigned long long pfg[kChunkFwd];
+#pragma unroll
+  for (int i = 0; i < kChunkFwd; ++i) pfg[i] = 0ull;
   const bool storer_mode = KR == 1 && DDR_FWD_STORER && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2;
   const bool storer_wave = storer_mode && wbase >= BS / 2;
   const int sr = tid - BS / 2;  // a storer thread's reach
@@ -577,7 +633,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // import the next chunk of every virtual inflow (x of the upstream block's reach): its owner
       // thread requests the kChunkFwd granules at once
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-      if (vown) {
+      if (kPrefImport && vown) {
+        // (light and medium loads) the chunk was requested one chunk ago: its granules have landed while
+        // the block ran, so the import waits only for those still unpublished, and the next chunk is
+        // requested now -- the owner's wave (and the barrier after it) no longer pays a memory round
+        // trip every kChunkFwd ticks
+        const int xi = a.xid ? a.xid[v_edge] : -1;  // split basin: another rank's block, receive rows
+        const double* row = xi >= 0 ? a.xfwd + (int64_t)xi * T : a.bnd + (int64_t)v_edge * T;
+        const int64_t t0 = (int64_t)tau - v_off;
+        double g[kChunkFwd];
+        if (xi >= 0) {
+          if (tau == 0) issue_granules<kChunkFwd, true>(row, t0, 0, T, pfg);
+          poll_granules<kChunkFwd, true>(row, t0, 0, T, pfg, g, a.status, bid, force_to);
+          issue_granules<kChunkFwd, true>(row, t0 + kChunkFwd, 0, T, pfg);
+        } else {
+          if (tau == 0) issue_granules<kChunkFwd, false>(row, t0, 0, T, pfg);
+          poll_granules<kChunkFwd, false>(row, t0, 0, T, pfg, g, a.status, bid, force_to);
+          issue_granules<kChunkFwd, false>(row, t0 + kChunkFwd, 0, T, pfg);
+        }
+#pragma unroll
+        for (int i = 0; i < kChunkFwd; ++i) ring[vi * kChunkFwd + i] = g[i];
+      } else if (vown) {
         // split basin: a cut edge from another rank's block arrives in this rank's receive rows
         const int xi = a.xid ? a.xid[v_edge] : -1;
         if (xi >= 0) {
