@@ -230,18 +230,25 @@ def setup_split(args, net, rank, world, dist, dev, T):
         dist.all_gather_object(res, (rank, handle))  # the split group's handle exchange (nothing to share)
         ok = torch.ones(1, device=dev)
     if split is not None:
-        try:  # hand-shake: a short forward on the split graph, every cross-rank edge exercised
+        try:  # hand-shake on the split graph, every cross-rank edge exercised
             from ddr_amd.ops import check_status
 
             if os.environ.get("DDR_SPLIT_FAIL_RANK") == str(rank):  # rehearsal of the fallback path
                 raise RuntimeError("simulated hand-shake failure (DDR_SPLIT_FAIL_RANK)")
 
-            Th = min(T, 48)
+            # a 720-step forward and backward: every cross-rank edge in both directions, over enough
+            # chunks to catch an intermittent hand-off (~1 % of a training step's work)
+            Th = min(T, 720)
             z = torch.full((n_loc,), 0.5, device=dev)
-            route(g, torch.full((Th, n_loc), 0.1, device=dev), z * 0.1, z, z * 10, z * 1000 + 1000, z * 0.01, z * 0.5,
-                  save=False, steps=Th)
-            check_status()
-            torch.cuda.synchronize()
+            zn = (z * 0.1).requires_grad_(True)
+            runoff, _, _, _ = route(g, torch.full((Th, n_loc), 0.1, device=dev), zn, z, z * 10, z * 1000 + 1000,
+                                    z * 0.01, z * 0.5, steps=Th, math=args.math)
+            runoff.backward(torch.ones_like(runoff))
+            check_status(True)
+            own = torch.from_numpy(split.owned_reaches).to(dev)  # the other ranks' rows are not this rank's
+            if not bool(torch.isfinite(runoff[own]).all()) or not bool(torch.isfinite(zn.grad[own]).all()):
+                raise RuntimeError("non-finite hand-shake outputs")
+            del runoff, zn
         except Exception as e:  # noqa: BLE001
             log(f"[rank {rank}] split-basin hand-shake failed ({e}); falling back to whole-basin sharding")
             ok.zero_()
