@@ -190,8 +190,8 @@ def cpu_baseline(args, net_global, x_const):
 
 def setup_split(args, net, rank, world, dist, dev, T):
     """C5 at N > 1: the largest outlet basin routed by a group of ranks (ddr_amd.split) when it exceeds
-    twice a rank's share, the other basins LPT-sharded over the remaining ranks.  A short hand-shake
-    launch checks the cross-rank path on this machine; if any rank fails it, every rank falls back to
+    twice a rank's share, the other basins LPT-sharded over the remaining ranks.  A hand-shake
+    launch checks the cross-rank path on this machine (against a whole-basin route of the same inputs); if any rank fails it, every rank falls back to
     whole-basin sharding (returns None; so does a plan without a split).  DDR_SPLIT_BASIN=0 disables, =force splits even at N = 2."""
     from ddr_amd.split import SplitBasin, block_edges, plan_block_ranks, plan_ranks, sub_network
 
@@ -237,18 +237,38 @@ def setup_split(args, net, rank, world, dist, dev, T):
                 raise RuntimeError("simulated hand-shake failure (DDR_SPLIT_FAIL_RANK)")
 
             # a 720-step forward and backward: every cross-rank edge in both directions, over enough
-            # chunks to catch an intermittent hand-off (~1 % of a training step's work)
+            # chunks to catch an intermittent hand-off (~1 % of a training step's work); the owned rows
+            # must equal a whole-basin route of the same inputs on this rank alone (partition-invariant)
             Th = min(T, 720)
+            gen = torch.Generator().manual_seed(20240611)
+            qp = (torch.rand((Th, n_loc), generator=gen) * 0.9 + 0.05).to(dev)
+            un = torch.rand(n_loc, generator=gen).to(dev)
             z = torch.full((n_loc,), 0.5, device=dev)
-            zn = (z * 0.1).requires_grad_(True)
-            runoff, _, _, _ = route(g, torch.full((Th, n_loc), 0.1, device=dev), zn, z, z * 10, z * 1000 + 1000,
-                                    z * 0.01, z * 0.5, steps=Th, math=args.math)
-            runoff.backward(torch.ones_like(runoff))
-            check_status(True)
+
+            def trial(graph):
+                zn = (un * 0.08 + 0.02).requires_grad_(True)
+                ro, _, _, _ = route(graph, qp, zn, z, z * 10, z * 1000 + 1000, z * 0.01, z * 0.5, steps=Th,
+                                    math=args.math)
+                ro.backward(torch.ones_like(ro))
+                check_status(True)
+                return ro.detach(), zn.grad
+
+            runoff, gn = trial(g)
             own = torch.from_numpy(split.owned_reaches).to(dev)  # the other ranks' rows are not this rank's
-            if not bool(torch.isfinite(runoff[own]).all()) or not bool(torch.isfinite(zn.grad[own]).all()):
+            runoff, gn = runoff[own], gn[own]
+            if not bool(torch.isfinite(runoff).all()) or not bool(torch.isfinite(gn).all()):
                 raise RuntimeError("non-finite hand-shake outputs")
-            del runoff, zn
+            gw = RiverGraph(n_loc, rows, cols, steps_hint=Th)
+            try:
+                r_w, g_w = trial(gw)
+            finally:
+                gw.close()
+            dr = float(((runoff - r_w[own]).abs() / r_w[own].abs().clamp_min(1e-30)).max())
+            dg = float((gn - g_w[own]).abs().max() / g_w[own].abs().max().clamp_min(1e-30))
+            log(f"[rank {rank}] split hand-shake vs whole-basin route: runoff max-rel {dr:.1e}, dL/dn {dg:.1e}")
+            if not (dr <= 1e-6 and dg <= 1e-5):
+                raise RuntimeError(f"hand-shake outputs differ from the whole-basin route ({dr:.1e}, {dg:.1e})")
+            del runoff, gn, r_w, g_w, qp
         except Exception as e:  # noqa: BLE001
             log(f"[rank {rank}] split-basin hand-shake failed ({e}); falling back to whole-basin sharding")
             ok.zero_()
