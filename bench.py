@@ -638,6 +638,9 @@ def time_training_stream(args, dev):
             g.close()  # the previous batch's graph: released stream-ordered after its launches
         g, m = next(pf)
         t_graph = time.perf_counter() - t0
+        # the host is off the critical path when it enqueues this step before the device has finished the
+        # previous one (the device then never waits for the host's graph)
+        ahead = bool(evs) and not evs[-1][1].query() if k > warm else None
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -655,7 +658,7 @@ def time_training_stream(args, dev):
         e1.record()
         if k >= warm:
             per.append({"reaches": int(d["net"].n), "generations": g.info.generations, "blocks": g.info.n_blocks,
-                        "graph_wait_ms": round(t_graph * 1e3, 2)})
+                        "graph_wait_ms": round(t_graph * 1e3, 2), "host_ahead": ahead})
             evs.append((e0, e1))
     torch.cuda.synchronize()
     timed = time.perf_counter() - t_start
@@ -670,6 +673,8 @@ def time_training_stream(args, dev):
             "graph_builder": args.stream_builder, "graph_workers": args.stream_workers,
             "graph_wait_ms_mean": float(np.mean(waits)) if waits else None,
             "step_gpu_ms_mean": gpu,
+            "host_ahead_steps": f"{sum(1 for b in per if b['host_ahead'])} of {sum(1 for b in per if b['host_ahead'] is not None)}"
+                                " (steps enqueued while the device was still on the previous step)",
             # wall time per step not inside a training step's own GPU span: the next batches' device
             # builds (queued between steps on the training stream) and any device idle time
             "between_steps_ms": timed / K * 1e3 - gpu,
