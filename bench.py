@@ -199,6 +199,7 @@ def setup_split(args, net, rank, world, dist, dev, T):
     ids_r, sp = plan[rank]
     any_split = any(s is not None for _, s in plan)
     if not any_split:
+        args.split_handshake = "no split planned"
         return None
     n_loc, rows, cols, ids = sub_network(net.n, net.rows, net.cols, ids_r)
     g = split = None
@@ -274,23 +275,31 @@ def setup_split(args, net, rank, world, dist, dev, T):
             ok.zero_()
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if ok.item() < 1:
+        args.split_handshake = "failed on some rank: whole-basin sharding"
         if g is not None:
             g.close()
         if split is not None:
             split.close()
         return None
+    args.split_handshake = "passed on every rank (owned rows equal a whole-basin route)"
     return g, split, n_loc, rows, cols, ids
 
 
-def counter_file(args, lib_hash):
+def counter_file(workload, T, lib_hash, reaches, world=1, split=None, root=ROOT):
     """PMC summary of this workload for the loaded library build (profiles/, made by tools/pmc.sh +
-    tools/pmc_to_json.py); None when absent or stale (another build or configuration)."""
-    f = ROOT / "profiles" / "counters" / f"{args.workload}.json"
+    tools/pmc_to_json.py); None when absent or stale: another build, T, or shard.  The counters describe
+    one launch over the reaches ONE process routed: they apply to a line only when this rank's shard is
+    the one measured -- the same reach count, world size and split role (``split`` = (index, k) of a
+    split-basin rank, else None).  The files measured on one GPU (world 1, the whole network) therefore
+    never label an N > 1 rank's line."""
+    f = Path(root) / "profiles" / "counters" / f"{workload}.json"
     try:
         d = json.loads(f.read_text())
     except (OSError, ValueError):
         return None
-    if d.get("build") != lib_hash or d.get("T") != args.T or d.get("reaches") != args.reaches_total:
+    if d.get("build") != lib_hash or d.get("T") != T or d.get("reaches") != reaches:
+        return None
+    if int(d.get("world", 1)) != int(world) or d.get("split") != (None if split is None else list(split)):
         return None
     return d
 
@@ -325,7 +334,8 @@ def main():
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
     ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
-                    help="forward coefficient arithmetic (default faithful, the drop-in's default; --fast-math = fast)")
+                    help="forward coefficient arithmetic (default faithful, the drop-in dmc's default -- "
+                         "MuskingumCunge(math) -- and what the trainer runs; --fast-math = fast)")
     args = ap.parse_args()
     args.math = args.math or ("fast" if args.fast_math else "faithful")
     spec = WORKLOADS[args.workload]
@@ -500,11 +510,20 @@ def main():
     # ---- reductions over ranks ------------------------------------------------------------------------
     sizes = torch.zeros(max(world, 1), device=dev, dtype=torch.float64)
     sizes[rank] = n_owned
+    # per rank: its routing kernels' mean ms (HIP events on the launch stream) and step ms
+    per = torch.zeros((max(world, 1), 3), device=dev, dtype=torch.float64)
+    per[rank, 0] = float(np.mean(kms["forward"])) if kms["forward"] else 0.0
+    per[rank, 1] = float(np.mean(kms["backward"])) if kms["backward"] else 0.0
+    per[rank, 2] = elapsed / args.steps * 1e3
     tmax = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    pg_world = 1
     if dist is not None:
         dist.all_reduce(sizes, op=dist.ReduceOp.SUM)
+        dist.all_reduce(per, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        pg_world = dist.get_world_size()
     sizes = sizes.cpu().numpy()
+    per = per.cpu().numpy()
     elapsed = float(tmax.item())
     total_reaches = int(sizes.sum())
     value = total_reaches * (T - 1) * args.steps / elapsed
@@ -522,7 +541,8 @@ def main():
             kern["backward"]["kernel_bytes_per_reach_step"] = bwd_kernel_bytes
         dom = max(kern, key=lambda k_: kern[k_]["kernel_ms"])
         achieved = kern[dom]["GB/s"]
-        cf = counter_file(args, lib_hash)
+        cf = counter_file(args.workload, args.T, lib_hash, n_owned, world,
+                          None if split is None else (split.index, split.k))
         kc = (cf or {}).get("kernels", {}).get(f"route_{dom}_kernel", {})
         dropin = None
         if args.workload == "c5" and world == 1 and args.dropin_steps > 0:
@@ -559,6 +579,12 @@ def main():
                        "split_basin": None if split is None else {"ranks": split.k, "cross_cut_edges": split.n_x,
                                                                   "receive_memory_kind": split.kind},
                        "reaches_per_rank": [int(s) for s in sizes],
+                       "world_size_process_group": pg_world if dist is not None else None,
+                       "per_rank_ms": None if dist is None else [
+                           {"rank": r_, "reaches": int(sizes[r_]), "forward_kernel_ms": round(float(per[r_, 0]), 3),
+                            "backward_kernel_ms": round(float(per[r_, 1]), 3) if spec["grad"] else None,
+                            "step_ms": round(float(per[r_, 2]), 3)} for r_ in range(world)],
+                       "split_handshake": getattr(args, "split_handshake", None),
                        "load_max_over_mean": float(sizes.max() / sizes.mean()),
                        "basin_bound_speedup": float(total_reaches / max(sizes.max(), largest))},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -87,6 +87,9 @@ _SIGS = {
     "ddr_graph_destroy": (C.c_int, [_P]),
     "ddr_graph_destroy_async": (C.c_int, [_P, _P]),
     "ddr_graph_upload": (C.c_int, [_P]),
+    "ddr_graph_upload_async": (C.c_int, [_P, _P]),
+    "ddr_graph_build_async": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P, C.POINTER(C.c_void_p)]),
+    "ddr_pool_trim": (C.c_int, [C.POINTER(C.c_int64)]),
     "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "ddr_collate_gauges_device": (C.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _I64, C.POINTER(C.c_int64), _P, _P,
                                             C.POINTER(C.c_int64), _P, _P, _P, _P, _I64, _P, _P]),
@@ -127,6 +130,7 @@ _SIGS = {
     "ddr_status_check": (C.c_int, [_I32]),
     "ddr_set_debug_flags": (C.c_int, [_I32]),
     "ddr_tri_solve": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _P]),
+    "ddr_tri_solve_ex": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _I32, _I32, _I32, _P]),
     "ddr_tri_grad_values": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P]),
     "ddr_set_kernel_timing": (C.c_int, [_I32]),
     "ddr_kernel_ms": (C.c_int, [_I32, C.POINTER(C.c_float)]),
@@ -151,7 +155,12 @@ def load() -> C.CDLL:
             f"libddr_mc.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C ddr_amd/csrc` (there is no CPU fallback)")
     lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+    # an explicitly chosen library (DDR_LIB / DDR_MC_LIB: an A/B variant of an earlier build) may lack
+    # entry points added since; the default in-tree library must export every one
+    variant = bool(os.environ.get("DDR_LIB") or os.environ.get("DDR_MC_LIB"))
     for name, (res, args) in _SIGS.items():
+        if variant and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

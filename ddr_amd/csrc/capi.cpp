@@ -207,6 +207,8 @@ ddr_status split_prepare(const Graph* g, RouteArgs& a, int64_t T, int slot, hipS
   a.xid = sp.xid;
   a.xcons = sp.xcons;
   a.xprod = sp.xprod;
+  a.xedge = sp.xedge;
+  a.xrank = sp.rank;
   auto rows = [&](char* base, int which) {
     double* f = reinterpret_cast<double*>(base + xmem_flags_bytes());
     return which == 0 ? f : f + sp.n_x * T;
@@ -248,6 +250,10 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   if (!x_save) return fail(DDR_ERR_ARG, "x_save is required (routing state, and the staging of runoff)");
   if (g->n_cut > 0 && !bnd) return fail(DDR_ERR_ARG, "graph has cut edges: bnd buffer required");
   if (!status) return fail(DDR_ERR_ARG, "null status block");
+  // a split basin's launches hand-shake per launch epoch with every peer: a launch only this rank makes
+  // (a hot start, the daily accumulation) would leave the epochs of all later launches off by one
+  if (g->split.nranks > 0 && (T < 2 || (flags & DDR_FWD_ACCUMULATE)))
+    return fail(DDR_ERR_ARG, "split basin: hot-start (T = 1) and accumulation launches are not supported");
   if ((st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, false))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
@@ -271,6 +277,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   DDR_HIP(timing_mark(0, 0, s));
   DDR_HIP(launch_route<R>(g, a, false, s));
   DDR_HIP(timing_mark(0, 1, s));
+  DDR_HIP(launch_split_finish<R>(g, a, s));
   // runoff (N, T) is written by the routing kernel itself (16-B row segments every 4 steps)
   return g_pending.enqueue(status, s, "forward", gh);
 }
@@ -358,6 +365,8 @@ ddr_status gauge_args(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   if (gz->n_gauges > 0 && (!gz->offsets || !gz->index)) return fail(DDR_ERR_ARG, "null gauge arrays");
   const Graph* g = reinterpret_cast<const Graph*>(gh);
   if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
+  // a split rank holds the states of its own blocks only: a gauge sum would read rows no launch wrote
+  if (g->split.nranks > 0) return fail(DDR_ERR_ARG, "split basin: gauge mode is not supported");
   std::memset(&a, 0, sizeof(a));
   a.s = g->dev;
   a.T = T;
@@ -540,9 +549,50 @@ ddr_status ddr_graph_upload(ddr_graph* g) {
   })
 }
 
+ddr_status ddr_graph_upload_async(ddr_graph* g, void* stream) {
+  DDR_GUARD({
+    if (!g) return fail(DDR_ERR_ARG, "null graph");
+    return upload_schedule_async(reinterpret_cast<Graph*>(g), static_cast<hipStream_t>(stream));
+  })
+}
+
+ddr_status ddr_graph_build_async(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                 const ddr_build_opts* opts, void* stream, ddr_graph** out) {
+  DDR_GUARD({
+    if (!out) return fail(DDR_ERR_ARG, "null out");
+    ddr_build_opts o;
+    std::memset(&o, 0, sizeof(o));
+    if (opts) o = *opts;
+    const bool host_only = o.flags & DDR_BUILD_HOST_ONLY;
+    o.flags |= DDR_BUILD_HOST_ONLY;
+    Graph* g = nullptr;
+    ddr_status st = build_graph(n, e, rows, cols, &o, &g);
+    if (st) return st;
+    if (!host_only && (st = upload_schedule_async(g, static_cast<hipStream_t>(stream)))) {
+      destroy_graph(g);
+      return st;
+    }
+    *out = reinterpret_cast<ddr_graph*>(g);
+    return DDR_OK;
+  })
+}
+
 ddr_status ddr_graph_destroy(ddr_graph* g) {
   DDR_GUARD({
-    destroy_graph(reinterpret_cast<Graph*>(g));
+    Graph* gr = reinterpret_cast<Graph*>(g);
+    // synchronous, as the header promises: the pooled blocks of a device-built graph go back to the pool
+    // only once no launch on any stream can still read them (their release event is recorded on the null
+    // stream, which does not order PyTorch's non-blocking streams)
+    if (gr && (gr->device_built || !gr->async_allocations.empty())) DDR_HIP(hipDeviceSynchronize());
+    destroy_graph(gr);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_pool_trim(int64_t* freed_bytes) {
+  DDR_GUARD({
+    const int64_t f = pool_trim();
+    if (freed_bytes) *freed_bytes = f;
     return DDR_OK;
   })
 }
@@ -659,12 +709,14 @@ ddr_status ddr_graph_set_split(ddr_graph* gh, int32_t rank, int32_t nranks, cons
     std::fill(xid.begin(), xid.end(), -1);
     std::vector<int32_t> xcons;
     std::vector<int32_t> xprod;
+    std::vector<int64_t> xedge;
     for (int64_t e = 0; e < g->n_cut; ++e) {
       if (prod[e] < 0 || cons[e] < 0) return fail(DDR_ERR_ARG, "split basin: cut edge without both blocks");
       if (block_rank[prod[e]] != block_rank[cons[e]]) {
         xid[e] = (int32_t)xcons.size();
         xcons.push_back(block_rank[cons[e]]);
         xprod.push_back(block_rank[prod[e]]);
+        xedge.push_back(e);
       }
     }
     std::vector<uint8_t> owned(nb);
@@ -680,6 +732,7 @@ ddr_status ddr_graph_set_split(ddr_graph* gh, int32_t rank, int32_t nranks, cons
     DDR_HIP(up(xid.data(), xid.size() * 4, reinterpret_cast<void**>(&sp.xid)));
     DDR_HIP(up(xcons.data(), xcons.size() * 4, reinterpret_cast<void**>(&sp.xcons)));
     DDR_HIP(up(xprod.data(), xprod.size() * 4, reinterpret_cast<void**>(&sp.xprod)));
+    DDR_HIP(up(xedge.data(), xedge.size() * 8, reinterpret_cast<void**>(&sp.xedge)));
     sp.rank = rank;
     sp.nranks = nranks;
     sp.n_x = (int32_t)xcons.size();

@@ -1,12 +1,12 @@
 // Per-reach temporal statistics of the trapezoid geometry over daily accumulated discharge
 // (reference src/ddr/geometry/statistics.py:20-83, driven by scripts/geometry_predictor.py:193-212).
 //
-// One wave per reach.  Lane l holds days l, l + 64, ..., (KD per lane, D <= 64 KD): it evaluates the
-// geometry of its days once (geometry/trapezoidal.py:62-97 in the routing kernels' exact operation
-// order, physics.h), then for each of the six variables (depth, top width, bottom width, side slope,
-// hydraulic radius, discharge) the wave sorts the D values (bitonic network: lane shuffles for
-// partners in other lanes, register swaps for partners in the same lane) and emits min, max, median
-// and mean.  NaN values are skipped like numpy's nanmin / nanmax / nanmedian / nanmean (a reach with
+// One wave per reach.  Lane l holds days l, l + 64, ..., (KD per lane, D <= 64 KD).  The wave sorts the
+// discharges once (bitonic network: lane shuffles for partners in other lanes, register swaps for
+// partners in the same lane), evaluates the geometry (geometry/trapezoidal.py:62-97 in the routing
+// kernels' exact operation order, physics.h) at the sorted discharges, and emits min, max, median and
+// mean of each of the six variables (depth, top width, bottom width, side slope, hydraulic radius,
+// discharge) from fixed positions where the variable is monotone in Q, else after sorting it.  NaN values are skipped like numpy's nanmin / nanmax / nanmedian / nanmean (a reach with
 // no valid day gets NaN).  The mean is accumulated in fp64 (numpy's pairwise fp32 sum differs in the
 // last bits).  Windows longer than 512 days (multi-year runs) take geometry_stats_long_kernel: one
 // workgroup per reach, the values sorted in LDS (up to kGeoLongMaxDays days).
@@ -81,6 +81,45 @@ __device__ __forceinline__ float wave_elem(const float (&v)[KD], int idx) {
   return __shfl(r, l, 64);
 }
 
+// The trapezoid geometry of one day (trapezoidal.py:62-97): coefficients<float, false>'s operations, in its
+// order, up to the hydraulic radius -- the statistics need no velocity and no Muskingum coefficients
+// (one pow and six divisions fewer per day than the routing step).  Bit-identical to the values
+// coefficients() computes on the way.
+struct DayGeom {
+  float depth, tw, bw, ss, Rh;
+};
+__device__ __forceinline__ DayGeom day_geometry(const ReachStatic<float>& s, float Q, const Consts<float>& c) {
+  DayGeom g;
+  const float num = (Q * s.n) * s.qe1();
+  const float ratio = dvf<false>(num, s.dd);
+  const float pwv = pwf<false>(ratio, s.expo, nullptr, c.pk);
+  g.depth = rmax(pwv, c.dlb);
+  const float dq = pwf<false>(g.depth, s.qe, nullptr, c.pk);
+  g.tw = s.p * dq;
+  const float ssr = dvf<false>(g.tw * s.qe, 2.0f * g.depth);
+  g.ss = rclamp(ssr, c.sslb, c.ssub);
+  const float bwr = g.tw - (2.0f * g.ss) * g.depth;
+  g.bw = rmax(bwr, c.bwlb);
+  const float area = ((g.tw + g.bw) * g.depth) * 0.5f;
+  const float sq = sqf<false>(1.0f + g.ss * g.ss);
+  const float wp = g.bw + (2.0f * g.depth) * sq;
+  g.Rh = dvf<false>(area, wp);
+  return g;
+}
+
+// The value of `var` (0 depth, 1 top width, 2 bottom width, 3 side slope, 4 hydraulic radius, 5 Q).
+__device__ __forceinline__ float geom_var(const DayGeom& g, float Q, int var) {
+  return var == 0 ? g.depth : (var == 1 ? g.tw : (var == 2 ? g.bw : (var == 3 ? g.ss : (var == 4 ? g.Rh : Q))));
+}
+
+// One wave per reach, days in Q order: the wave sorts the valid discharges once (bitonic, NaN last), then
+// evaluates each day's geometry at the sorted Q (the geometry is a function of Q alone), so element e of
+// every variable belongs to the e-th smallest discharge.  A variable whose values are monotone along that
+// order (the common case: depth and top width are non-decreasing in Q, the others nearly always monotone
+// over one reach's year) has its order statistics at fixed positions; the wave checks monotonicity on
+// every adjacent pair and sorts only a variable that is not (or has a NaN where Q is valid).  Exact:
+// the same min / max / median as a sort of every variable, in every case.  The mean is the fp64 sum of
+// the valid values (fp32 values, so the order does not change it where the range stays within 2^29).
 template <int KD>
 __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
   load_math_tables();
@@ -102,49 +141,84 @@ __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
   // trapezoidal.py:62-66: the static part (no length / storage enter the geometry)
   const ReachStatic<float> st = make_static<float>(a.n[reach], a.q[reach], a.p[reach * a.p_stride], a.S[reach],
                                                    1.0f, 0.0f);
-  float vals[kGeoVars][KD];
+  float qv[KD];
+  int cq = 0;
 #pragma unroll
   for (int i = 0; i < KD; ++i) {
     const int64_t d = (int64_t)i * 64 + lane;
     const float Q = d < a.D ? a.qd[reach * a.rs + d * a.ds] : __builtin_nanf("");
-    float c1, c2, c3, c4, tw, ss;
-    Geom<float> g;
-    coefficients<float, false>(st, Q, cs, c1, c2, c3, c4, tw, ss, &g);
-    const bool ok = d < a.D && Q == Q;  // torch propagates a NaN discharge through every variable
-    vals[0][i] = ok ? g.depth : __builtin_nanf("");
-    vals[1][i] = ok ? g.tw : __builtin_nanf("");
-    vals[2][i] = ok ? g.bw : __builtin_nanf("");
-    vals[3][i] = ok ? g.ss : __builtin_nanf("");
-    vals[4][i] = ok ? g.Rh : __builtin_nanf("");
-    vals[5][i] = Q;
+    const bool valid = Q == Q;  // torch propagates a NaN discharge through every variable
+    cq += valid;
+    qv[i] = valid ? Q : __builtin_inff();  // NaN (and the padding) sorts last, past the valid count
   }
 #pragma unroll
+  for (int m = 1; m < 64; m <<= 1) cq += __shfl_xor(cq, m, 64);
+  wave_sort<KD>(qv, lane);
+  float vals[kGeoVars][KD];
+#pragma unroll
+  for (int i = 0; i < KD; ++i) {
+    const bool ok = i * 64 + lane < cq;
+    const float Q = ok ? qv[i] : 1.0f;  // (padding: any positive value, the result is discarded)
+    const DayGeom g = day_geometry(st, Q, cs);
+#pragma unroll
+    for (int var = 0; var < kGeoVars; ++var) vals[var][i] = ok ? geom_var(g, Q, var) : __builtin_nanf("");
+  }
+#pragma unroll 1
   for (int var = 0; var < kGeoVars; ++var) {
     float v[KD];
     int cnt = 0;
     double sum = 0.0;
+    bool inc = true, dec = true;
 #pragma unroll
     for (int i = 0; i < KD; ++i) {
       const float x = vals[var][i];
       const bool valid = x == x;
       cnt += valid;
       sum += valid ? (double)x : 0.0;
-      v[i] = valid ? x : __builtin_inff();  // NaN sorts last, past the valid count
+      v[i] = x;
     }
-    // wave totals (every lane ends with the same value)
+    // adjacent pairs (e, e + 1), e + 1 < cq: element e + 1 is lane + 1's v[i] (lane 0's v[i + 1] for lane 63)
+#pragma unroll
+    for (int i = 0; i < KD; ++i) {
+      const float s0 = __shfl(v[i], (lane + 1) & 63, 64);
+      const float s1 = i + 1 < KD ? __shfl(v[i + 1], 0, 64) : 0.0f;
+      const float nb = lane < 63 ? s0 : s1;
+      const bool pair = i * 64 + lane + 1 < cq;
+      inc = inc && (!pair || v[i] <= nb);
+      dec = dec && (!pair || v[i] >= nb);
+    }
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
       cnt += __shfl_xor(cnt, m, 64);
       sum += __shfl_xor(sum, m, 64);
     }
-    wave_sort<KD>(v, lane);
+    const bool all_inc = __builtin_amdgcn_ballot_w64(!inc) == 0;
+    const bool all_dec = __builtin_amdgcn_ballot_w64(!dec) == 0;
     float mn, mx, med, mean;
     if (cnt == 0) {
       mn = mx = med = mean = __builtin_nanf("");
     } else {
-      mn = wave_elem<KD>(v, 0);
-      mx = wave_elem<KD>(v, cnt - 1);
-      const float lo = wave_elem<KD>(v, (cnt - 1) / 2), hi = wave_elem<KD>(v, cnt / 2);
+      int i_mn, i_mx, i_lo, i_hi;  // positions of the order statistics among elements [0, cnt)
+      if (cnt == cq && (all_inc || all_dec)) {
+        const bool up = all_inc;
+        auto at = [&](int j) { return up ? j : cnt - 1 - j; };  // j-th smallest
+        i_mn = at(0);
+        i_mx = at(cnt - 1);
+        i_lo = at((cnt - 1) / 2);
+        i_hi = at(cnt / 2);
+      } else {
+        // not monotone along Q (or NaN where Q is valid): sort this variable
+#pragma unroll
+        for (int i = 0; i < KD; ++i) v[i] = v[i] == v[i] ? v[i] : __builtin_inff();
+        wave_sort<KD>(v, lane);
+        i_mn = 0;
+        i_mx = cnt - 1;
+        i_lo = (cnt - 1) / 2;
+        i_hi = cnt / 2;
+      }
+      mn = wave_elem<KD>(v, i_mn);
+      mx = wave_elem<KD>(v, i_mx);
+      const float lo = wave_elem<KD>(v, i_lo), hi = wave_elem<KD>(v, i_hi);
       med = (cnt & 1) ? lo : (lo + hi) / 2.0f;  // numpy: mean of the two middle values
       mean = (float)(sum / (double)cnt);
     }

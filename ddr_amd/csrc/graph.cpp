@@ -20,6 +20,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <cmath>
 #include <memory>
 #include <mutex>
@@ -43,6 +44,67 @@ ddr_status upload(Graph* g, T** dst, const std::vector<T>& src) {
 }
 
 }  // namespace
+
+// Stream-ordered upload (ddr_graph_build_async / ddr_graph_upload_async): every schedule array is packed
+// into one pinned staging block and one pooled device block, one copy on `stream`, and the graph's ready
+// event recorded behind it -- routing launches on any stream wait for that event (graph_ready); no
+// device-wide synchronisation (hipMalloc / hipMemcpy of pageable memory have one each).
+ddr_status upload_schedule_async(Graph* g, hipStream_t stream) {
+  if (g->uploaded) return DDR_OK;
+  HostSchedule& H = g->hs;
+  DevSchedule& D = g->dev;
+  size_t total = 0;
+  auto room = [&](size_t n, size_t elem) { total = align16(total) + std::max<size_t>(n, 1) * elem; };
+  room(g->blocks.size(), sizeof(BlockDesc));
+  for (const std::vector<int32_t>* v : {&H.ref, &H.off, &H.upb, &H.upc, &H.dloc, &H.cut, &H.uplist, &H.xoff,
+                                        &H.xlist, &H.v_edge, &H.v_off, &H.v_dloc, &H.cout_loc, &H.pos_of_ref,
+                                        &H.block_of_pos, &H.rs_loc, &H.rs_ref})
+    room(v->size(), sizeof(int32_t));
+  total = align16(total);
+  unsigned char* host = static_cast<unsigned char*>(pinned_get(total));
+  if (!host) return fail(DDR_ERR_HIP, "graph upload: pinned host memory");
+  unsigned char* dev = static_cast<unsigned char*>(device_get(total, stream));
+  if (!dev) {
+    pinned_put(host, stream);
+    return fail(DDR_ERR_HIP, "graph upload: out of device memory");
+  }
+  g->staging = host;
+  g->async_allocations.push_back(dev);
+  size_t o = 0;
+  auto place = [&](const void* src, size_t n, size_t elem) {
+    o = align16(o);
+    if (n) std::memcpy(host + o, src, n * elem);
+    void* d = dev + o;
+    o += std::max<size_t>(n, 1) * elem;
+    return d;
+  };
+  D.blocks = static_cast<BlockDesc*>(place(g->blocks.data(), g->blocks.size(), sizeof(BlockDesc)));
+  auto put = [&](int32_t** dst, const std::vector<int32_t>& v) { *dst = static_cast<int32_t*>(place(v.data(), v.size(), 4)); };
+  put(&D.ref, H.ref);
+  put(&D.off, H.off);
+  put(&D.upb, H.upb);
+  put(&D.upc, H.upc);
+  put(&D.dloc, H.dloc);
+  put(&D.cut, H.cut);
+  put(&D.uplist, H.uplist);
+  put(&D.xoff, H.xoff);
+  put(&D.xlist, H.xlist);
+  put(&D.v_edge, H.v_edge);
+  put(&D.v_off, H.v_off);
+  put(&D.v_dloc, H.v_dloc);
+  put(&D.cout_loc, H.cout_loc);
+  put(&D.pos_of_ref, H.pos_of_ref);
+  put(&D.block_of_pos, H.block_of_pos);
+  put(&D.rs_loc, H.rs_loc);
+  put(&D.rs_ref, H.rs_ref);
+  DDR_HIP(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, stream));
+  if (!g->ready) DDR_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
+  DDR_HIP(hipEventRecord(g->ready, stream));
+  DDR_HIP(hipGetDevice(&g->device));
+  g->uploaded = true;
+  g->hs = HostSchedule{};
+  return DDR_OK;
+}
 
 ddr_status upload_schedule(Graph* g) {
   if (g->uploaded) return DDR_OK;
@@ -265,7 +327,9 @@ ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* ou
     mc = std::max(mc, bc[b]);
     mx = std::max(mx, bx[b]);
   }
-  const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4),
+  int64_t maxl = 0;
+  for (int64_t b = 0; b < nblocks; ++b) maxl = std::max(maxl, load[b]);
+  const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4, fwd_xbuf(kr_of_load(maxl))),
                                route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
   if (P.dbg) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
   // (a count failure at the capacity ceiling of the unweighted packing goes to more generations:
@@ -349,9 +413,7 @@ ddr_status finalize_blocks(Graph* g, const PackPlan& P, const PackResult& R) {
   g->sum_dn = pre_dn;
   g->max_nloc = (int)max_load;
   g->n_xlist = x0;
-  int kr = 1;
-  while (int64_t(kr) * kBlockThreads < max_load) kr *= 2;
-  g->kr = kr;
+  g->kr = kr_of_load(max_load);
   if (g->max_virt > kBlockThreads || g->max_cout > kBlockThreads)
     return fail(DDR_ERR_CAPACITY, "too many inter-workgroup edges in one workgroup");
   return DDR_OK;
@@ -660,8 +722,9 @@ void destroy_graph(Graph* g, hipStream_t stream) {
 }
 
 namespace {
-// One pool for pinned host blocks (device = -1) and device blocks (device id).  Blocks are never
-// freed (hipHostFree and hipFree synchronise with the device); sizes are power-of-two classes.
+// One pool for pinned host blocks (device = -1) and device blocks (device id).  Blocks are kept for reuse
+// (hipHostFree and hipFree synchronise with the device) until ddr_pool_trim releases the idle ones; sizes
+// are rounded up to classes of 8 steps per power of two (at most 1/8 over the request past 2 KiB).
 struct PoolBlock {
   void* p = nullptr;
   size_t bytes = 0;
@@ -673,9 +736,15 @@ std::mutex g_pool_mu;
 std::vector<PoolBlock> g_pool;
 
 size_t size_class(size_t bytes) {
-  size_t cls = 256;
-  while (cls < bytes) cls <<= 1;
-  return cls;
+  if (bytes <= 2048) {
+    size_t cls = 256;
+    while (cls < bytes) cls <<= 1;
+    return cls;
+  }
+  size_t top = 2048;
+  while (top * 2 < bytes) top <<= 1;  // top < bytes <= 2 top
+  const size_t step = top / 8;
+  return (bytes + step - 1) / step * step;
 }
 
 void pool_put(void* p, hipStream_t s) {
@@ -738,5 +807,24 @@ void* device_get(size_t bytes, hipStream_t s) {
   return p;
 }
 void device_put(void* p, hipStream_t s) { pool_put(p, s); }
+
+int64_t pool_trim() {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int64_t freed = 0;
+  std::vector<PoolBlock> keep;
+  for (PoolBlock& b : g_pool) {
+    // a block handed out, or one whose last user's queued work has not finished, stays
+    if (b.out || (b.ev && hipEventQuery(b.ev) != hipSuccess)) {
+      keep.push_back(b);
+      continue;
+    }
+    if (b.ev) (void)hipEventDestroy(b.ev);
+    if (b.device < 0) (void)hipHostFree(b.p);
+    else (void)hipFree(b.p);
+    freed += (int64_t)b.bytes;
+  }
+  g_pool.swap(keep);
+  return freed;
+}
 
 }  // namespace ddr

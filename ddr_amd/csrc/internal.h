@@ -55,9 +55,22 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) / 16 * 16;
 // LDS slots per buffer of the routing kernels: every block's nloc + nvirt slots, one zero slot
 // (missing upstreams of the forward read it), rounded up to even (16-B aligned statics rows).
 __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_slots + 2) & ~1; }
+// Forward x slots double-buffered by tick parity at KR <= 2 (one workgroup barrier per tick instead of
+// two: a tick's results go straight into the other buffer; the LDS is there at one or two reaches per
+// thread, not at four)
+#ifndef DDR_FWD_DBL
+#define DDR_FWD_DBL 1
+#endif
+__host__ __device__ constexpr int fwd_xbuf(int kr) { return (DDR_FWD_DBL && kr <= 2) ? 2 : 1; }
+// reaches per thread of the routing kernels for a largest block of `max_load` reaches
+inline int kr_of_load(int64_t max_load) {
+  int kr = 1;
+  while (int64_t(kr) * kBlockThreads < max_load) kr *= 2;
+  return kr;
+}
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
-//   forward : x slots (f64) | 6 statics (R) | ring [nvirt][kChunkFwd] f64
+//   forward : x slots (f64, xbuf buffers) | 6 statics (R) | ring [nvirt][kChunkFwd] f64
 //   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunkBwd][2] (R)
 //             | owner words
 // and then the block's confluence lists (after the math tables of fastmath.h, which occupy the first
@@ -67,8 +80,8 @@ constexpr size_t kMathTabBytes = 3072;
 // kMaxConfluenceList int32 entries per block (13-bit offsets in the packed upstream word).
 constexpr int kMaxConfluenceList = 8191;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nvirt, size_t ncout, size_t nxl, bool backward,
-                                                  size_t rsize) {
-  const size_t base = backward ? slots * 9 * rsize : slots * (8 + 6 * rsize);
+                                                  size_t rsize, int xbuf = 1) {
+  const size_t base = backward ? slots * 9 * rsize : slots * (8 * (size_t)xbuf + 6 * rsize);
   const size_t ring = backward ? ncout * kChunkBwd * 2 * rsize : nvirt * kChunkFwd * 8;
   // backward: per hand-off owner thread (tid < max(nvirt, ncout)) its virtual's downstream slot and
   // its cut-out's tick offset
@@ -145,6 +158,7 @@ struct SplitState {
   int32_t* xid = nullptr;    // device (n_cut): index among the cross-rank cut edges, -1 = local
   int32_t* xcons = nullptr;  // device (n_x): rank of the consumer (downstream) block
   int32_t* xprod = nullptr;  // device (n_x): rank of the producer (upstream) block
+  int64_t* xedge = nullptr;  // device (n_x): the cut edge of each cross-rank index
   char* local = nullptr;     // this rank's receive block
   char* peers[kMaxSplitRanks] = {};
   unsigned long long epoch[2] = {0, 0};
@@ -243,6 +257,9 @@ void pinned_put(void* p, hipStream_t s);
 // returned; device_put(p, s) returns it after the work queued on `s` so far.  hipMalloc only grows.
 void* device_get(size_t bytes, hipStream_t s);
 void device_put(void* p, hipStream_t s);
+// Releases every pooled block (pinned and device) that is not handed out and whose last user's work has
+// finished; returns the bytes freed (ddr_pool_trim)
+int64_t pool_trim();
 
 // graph.cpp
 ddr_status build_graph(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
@@ -277,6 +294,7 @@ ddr_status device_views_to_host(const Graph* g, int64_t* crow, int64_t* col, int
 ddr_status device_schedule_to_host(const Graph* g, HostSchedule& H);
 // Upload a host-built schedule (DDR_BUILD_HOST_ONLY) to the current device; no-op once uploaded.
 ddr_status upload_schedule(Graph* g);
+ddr_status upload_schedule_async(Graph* g, hipStream_t stream);
 
 // Status block layout (device, zeroed before every launch): word 0 = timed-out hand-offs, word 1 =
 // first failing block + 1, word 2 = forward ticket counter, word 3 = backward ticket counter.

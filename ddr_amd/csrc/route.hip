@@ -439,9 +439,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
-  double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [S] x_j(t), solve precision
-  const StatTab<R> tab{reinterpret_cast<R*>(sx + S)};                   // [S][6]
-  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 + 6 * sizeof(R))));  // [nvirt][kChunkFwd]
+  // kDbl: [2][S] x slots by tick parity -- tick tau reads buffer (tau - 1) & 1 and writes its results
+  // straight into buffer tau & 1, one workgroup barrier per tick; else [S], written in a publish phase
+  // between two barriers
+  constexpr int kXBuf = fwd_xbuf(KR);
+  constexpr bool kDbl = kXBuf == 2;
+  double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [kXBuf][S] x_j(t), solve precision
+  const StatTab<R> tab{reinterpret_cast<R*>(sx + kXBuf * S)};           // [S][6]
+  double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 * kXBuf + 6 * sizeof(R))));  // [nvirt][kChunkFwd]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
   const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith);
   const int64_t T = a.T;
@@ -517,6 +522,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if constexpr (kStatReg) sreg[k] = tab.get_pre(hk ? r : 0, st.expo, st.inv_n);  // the values the LDS path reads
   }
   if (tid == 0) sx[S - 1] = 0.0;
+  if (kDbl && tid == 0) sx[2 * S - 1] = 0.0;
 #ifndef DDR_FWD_VOWN_HIGH
 #define DDR_FWD_VOWN_HIGH 1
 #endif
@@ -576,7 +582,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const int so = opq(soff);
     const int t = taup - (so & 0xFFFF);
     if (t < 0 || t >= T) return;
-    const double xd = sx[sr];
+    const double xd = sx[(kDbl ? (taup & 1) * S : 0) + sr];
     const R xr = R(xd);
     if (DDR_FWD_STORER_GRANULES && B.ncout > 0 && (so >> 16)) {
       const int64_t e = B.cout0 + (so >> 16) - 1;
@@ -689,6 +695,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     prefetch(tau + 1, qnext, tq, sc);
     R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
+    const double* sxr = sx + (kDbl ? ((tau + 1) & 1) * S : 0);  // the slots published at tick tau - 1
+    double* sxw = sx + (kDbl ? (tau & 1) * S : 0);              // (kDbl) this tick's results
     // ---- compute, NP slices at a time: their physics in lockstep (NP independent dependency
     //      chains per wave: the tick is latency-bound at 4 waves per SIMD), then per slice the
     //      fp64 column sweep and the stores -------------------------------------------------------
@@ -740,8 +748,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
         const R qc = rmax(qv, cs.qlb);                                        // mmc.py:421-424
         const R b = ((ph[h].c2 * In[k]) + (ph[h].c3 * Q[k])) + (ph[h].c4 * qc);  // mmc.py:535-538
-        const double x0v = sx[up_0(up[k])];
-        const double x1v = sx[up_1(up[k], xl)];
+        const double x0v = sxr[up_0(up[k])];
+        const double x1v = sxr[up_1(up[k], xl)];
         // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
         const bool raw = !kSt && (t == 0 && carry);
         auto qf = [&](double x) -> R {
@@ -765,7 +773,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           const int* lst = xl + up_f1(up[k]);
           const int c = lst[0];
           for (int j = 2; j < c; ++j) {
-            const double xj = sx[lst[j]];
+            const double xj = sxr[lst[j]];
             acc = acc + dc1 * xj;
             if constexpr (!kSt) hot = hot + xj;
             inn = inn + qf(xj);
@@ -773,6 +781,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         }
         const double x = kSt ? acc : ((t == 0 && carry) ? (double)qcur[k] : ((t == 0 || accum) ? hot : acc));
         xk[k] = x;
+        if (kDbl && hk && (kSt || (t >= 0 && t < T))) sxw[r] = x;  // published: read at tick tau + 1
         if (hk && (kSt || (t >= 0 && t < T))) {
           const R xr = R(x);
           const R Qn = raw ? xr : rmax_nan(xr, cs.qlb);
@@ -809,6 +818,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         }
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (kDbl) {
+      // the virtual inflows' values of this tick, beside the reaches' (owners only read their own ring)
+      if (vown) {
+        const int t = tau - v_off;
+        if (t >= 0 && t < T) sxw[B.nloc + vi] = ring[vi * kChunkFwd + (tau % kChunkFwd)];
+      }
+      phz.mark(2);  // prefetch issue + compute + publish
+      lds_barrier();
+      phz.mark(3);  // the tick's one barrier
+      return;
     }
     phz.mark(2);  // prefetch issue + compute
     lds_barrier();
@@ -894,6 +914,13 @@ __global__ void __launch_bounds__(256) route_last_kernel(RouteArgs a) {
   const int64_t off = a.s.off[P];
   const int ref = a.s.ref[P];
   const int64_t T = a.T;
+  if (a.owned && !a.owned[a.s.block_of_pos[P]]) {  // split basin: another rank routes this reach
+    const R nan = R(__builtin_nan(""));
+    if (a.q_last) static_cast<R*>(a.q_last)[ref] = nan;
+    if (a.tw_last) static_cast<R*>(a.tw_last)[ref] = nan;
+    if (a.ss_last) static_cast<R*>(a.ss_last)[ref] = nan;
+    return;
+  }
   const R* xs = static_cast<const R*>(a.x_save) + T * B.pos0 + B.pre_dn;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool accum = a.flags & DDR_FWD_ACCUMULATE;
@@ -1083,10 +1110,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
   // x of a virtual inflow (the upstream reach of cut edge v_edge) at step t, from the forward's
   // boundary granules (t clamped into [0, T))
+  // split basin: a virtual whose producer is another rank's block sends its x to this rank's receive rows;
+  // split_finish_kernel copied them into this call's bnd after the forward
   const int vxi = (vown && a.xid) ? a.xid[v_edge] : -1;  // split basin: the virtual's cross-rank row
   auto load_virt = [&](int64_t t) -> double {
     const int64_t tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
-    if (vxi >= 0) return __longlong_as_double(load_granule_sys(a.xfwd + (int64_t)vxi * T + tc));
     return a.bnd[(int64_t)v_edge * T + tc];
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
@@ -1678,7 +1706,7 @@ __global__ void gauge_daily_seed_kernel(int64_t G, int64_t T, int64_t t0, int64_
 template <typename R>
 size_t route_smem_bytes(const Graph* g, bool backward) {
   return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt, (size_t)g->max_cout,
-                         (size_t)g->max_xl, backward, sizeof(R));
+                         (size_t)g->max_xl, backward, sizeof(R), fwd_xbuf(g->kr));
 }
 
 // Split basin: after the layout, each block's granule rows (tagged pointers, bit 0 = another rank's
@@ -1789,6 +1817,35 @@ hipError_t launch_split_barrier(const SplitBarrierArgs& b, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// Split basin, after the forward (grid-stride over n_x rows x T): rows received from another rank
+// (xcons == this rank) -> bnd[edge] (the per-call boundary buffer the autograd node keeps; a later forward
+// on the same graph resets and rewrites the receive rows); and a NaN in column 0 of every runoff row of a
+// reach whose block another rank runs (those rows are never written: misuse shows as NaN, not as stale
+// memory).  The last-step outputs of those reaches are NaN as well (route_last_kernel).
+template <typename R>
+__global__ void split_finish_kernel(RouteArgs a, int64_t n_x) {
+  const int64_t T = a.T;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_x * T; w += stride) {
+    const int64_t xi = w / T, t = w % T;
+    if (a.xcons[xi] != a.xrank) continue;
+    a.bnd[a.xedge[xi] * T + t] = __longlong_as_double(load_granule_sys(a.xfwd + w));
+  }
+  if (a.runoff) {
+    for (int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; P < a.N; P += stride)
+      if (!a.owned[a.s.block_of_pos[P]]) static_cast<R*>(a.runoff)[(int64_t)a.s.ref[P] * T] = R(__builtin_nan(""));
+  }
+}
+
+template <typename R>
+hipError_t launch_split_finish(const Graph* g, const RouteArgs& a, hipStream_t stream) {
+  if (g->split.nranks == 0) return hipSuccess;
+  const int64_t work = std::max<int64_t>((int64_t)g->split.n_x * a.T, g->n);
+  const unsigned nb = (unsigned)std::min<int64_t>((work + 255) / 256, 4096);
+  hipLaunchKernelGGL(split_finish_kernel<R>, dim3(nb), dim3(256), 0, stream, a, (int64_t)g->split.n_x);
+  return hipGetLastError();
+}
+
 template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream) {
   if (g->max_nloc == 0 || a.T == 0) return hipSuccess;
@@ -1863,6 +1920,8 @@ template hipError_t launch_route<float>(const Graph*, const RouteArgs&, bool, hi
 template hipError_t launch_route<double>(const Graph*, const RouteArgs&, bool, hipStream_t);
 template int max_resident_blocks<float>(const Graph*, bool);
 template int max_resident_blocks<double>(const Graph*, bool);
+template hipError_t launch_split_finish<float>(const Graph*, const RouteArgs&, hipStream_t);
+template hipError_t launch_split_finish<double>(const Graph*, const RouteArgs&, hipStream_t);
 template hipError_t launch_gather_qprime<float>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_gather_qprime<double>(const Graph*, RouteArgs&, hipStream_t);
 template hipError_t launch_scatter_qprime_grad<float>(const Graph*, const RouteArgs&, int64_t, float*, hipStream_t);

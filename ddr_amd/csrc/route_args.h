@@ -60,6 +60,8 @@ struct RouteArgs {
   const int32_t* xid;
   const int32_t* xcons;
   const int32_t* xprod;
+  const int64_t* xedge;
+  int32_t xrank;  // this rank's index in the split group
   double* xfwd;
   double* xbwd;
   double* pxfwd[kMaxSplitRanks];
@@ -93,6 +95,11 @@ struct SplitBarrierArgs {
   unsigned* status;
 };
 hipError_t launch_split_barrier(const SplitBarrierArgs& b, hipStream_t stream);
+// split basin, after a forward: the cross-rank x rows this rank received are copied into the call's own
+// boundary buffer (the backward reads them there, never from the shared receive rows a later forward
+// overwrites), and column 0 of the runoff rows of reaches another rank routes is set to NaN
+template <typename R>
+hipError_t launch_split_finish(const Graph* g, const RouteArgs& a, hipStream_t stream);
 // dL/dq' (rows of the caller's store, (rows, N)) from the state-gradient backward's gqs: the adjoint
 // of gather_qprime (sum over the steps reading each row, times flow_scale, 0 for a filled divide)
 template <typename R>

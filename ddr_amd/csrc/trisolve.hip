@@ -21,11 +21,15 @@ __global__ void __launch_bounds__(1024) tri_solve_kernel(int64_t n, const int64_
                                                          const int64_t* edep, const int64_t* eval,
                                                          const int64_t* diag_k, const float* values,
                                                          const float* b, double* y, float* x,
-                                                         unsigned* singular) {
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const int64_t k = diag_k[i];
-    const float d = k >= 0 ? values[k] : 0.0f;
-    if (d == 0.0f) atomicOr(singular, 1u);
+                                                         unsigned* singular, int unit) {
+  // unit diagonal (SciPy: A.setdiag(1), no diag^-1 scaling): the stored diagonal is never read
+  auto invd = [&](int64_t j) { return unit ? 1.0 : 1.0 / (double)values[diag_k[j]]; };
+  if (!unit) {
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const int64_t k = diag_k[i];
+      const float d = k >= 0 ? values[k] : 0.0f;
+      if (d == 0.0f) atomicOr(singular, 1u);
+    }
   }
   __syncthreads();
   for (int64_t l = 0; l < nlvl; ++l) {
@@ -34,7 +38,7 @@ __global__ void __launch_bounds__(1024) tri_solve_kernel(int64_t n, const int64_
       double acc = (double)b[i];
       for (int64_t e = eptr[i]; e < eptr[i + 1]; ++e) {
         const int64_t j = edep[e];
-        const double invd_j = 1.0 / (double)values[diag_k[j]];
+        const double invd_j = invd(j);
         const double lij = (double)values[eval[e]] * invd_j;
         acc = acc - lij * y[j];
       }
@@ -43,8 +47,7 @@ __global__ void __launch_bounds__(1024) tri_solve_kernel(int64_t n, const int64_
     __syncthreads();
   }
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const double invd = 1.0 / (double)values[diag_k[i]];
-    x[i] = (float)(y[i] * invd);
+    x[i] = unit ? (float)y[i] : (float)(y[i] * invd(i));
   }
 }
 
@@ -69,7 +72,7 @@ namespace {
 // plans are cached by a hash of the pattern: a repeated call uploads nothing and allocates nothing.
 struct TriPlan {
   int64_t n = 0, nnz = 0, nlvl = 0, ndep = 0;
-  int lower = 0, transpose = 0, device = -1;
+  int lower = 0, transpose = 0, unit = 0, device = -1;
   uint64_t hash = 0;
   std::vector<int64_t> crow, col;  // the pattern itself (a hash match is confirmed exactly)
   char* dev = nullptr;             // lvl_ptr | order | eptr | edep | eval | diag | y (f64) | flag
@@ -110,8 +113,9 @@ ddr_status build_plan(TriPlan& P, const int64_t* crow, const int64_t* col) {
       deps[r].push_back({c, k});
     }
   }
-  for (int64_t i = 0; i < n; ++i)
-    if (diag_k[i] < 0) return fail(DDR_ERR_SINGULAR, "A is singular: zero entry on diagonal");
+  if (!P.unit)
+    for (int64_t i = 0; i < n; ++i)
+      if (diag_k[i] < 0) return fail(DDR_ERR_SINGULAR, "A is singular: zero entry on diagonal");
   // SciPy column sweep order: lower -> ascending dependency, upper -> descending dependency
   for (auto& d : deps)
     std::sort(d.begin(), d.end(), [&](auto a, auto c) { return eff_lower ? a.first < c.first : a.first > c.first; });
@@ -153,7 +157,7 @@ ddr_status build_plan(TriPlan& P, const int64_t* crow, const int64_t* col) {
 
 // Cached plan for this pattern on the current device (built on a miss).
 ddr_status get_plan(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col, int lower, int transpose,
-                    std::shared_ptr<TriPlan>* out) {
+                    int unit, std::shared_ptr<TriPlan>* out) {
   int device = 0;
   DDR_HIP(hipGetDevice(&device));
   const uint64_t h = hash_pattern(crow, col, n, nnz);
@@ -162,7 +166,7 @@ ddr_status get_plan(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* 
     for (size_t i = 0; i < g_plans.size(); ++i) {
       const auto& P = g_plans[i];
       if (P->hash == h && P->n == n && P->nnz == nnz && P->lower == lower && P->transpose == transpose &&
-          P->device == device && std::equal(crow, crow + n + 1, P->crow.begin()) &&
+          P->unit == unit && P->device == device && std::equal(crow, crow + n + 1, P->crow.begin()) &&
           std::equal(col, col + nnz, P->col.begin())) {
         *out = P;
         std::rotate(g_plans.begin() + i, g_plans.begin() + i + 1, g_plans.end());  // most recent last
@@ -175,6 +179,7 @@ ddr_status get_plan(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* 
   P->nnz = nnz;
   P->lower = lower;
   P->transpose = transpose;
+  P->unit = unit;
   P->device = device;
   P->hash = h;
   P->crow.assign(crow, crow + n + 1);
@@ -191,14 +196,15 @@ ddr_status get_plan(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* 
 }  // namespace
 }  // namespace ddr
 
-extern "C" ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
-                                    const float* values, const float* b, float* x, int32_t lower,
-                                    int32_t transpose, void* stream) {
+extern "C" ddr_status ddr_tri_solve_ex(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
+                                       const float* values, const float* b, float* x, int32_t lower,
+                                       int32_t transpose, int32_t unit_diagonal, void* stream) {
   try {
     if (n <= 0 || !crow || (nnz > 0 && !col) || !values || !b || !x) return fail(DDR_ERR_ARG, "bad tri_solve args");
     if (crow[0] != 0 || crow[n] != nnz) return fail(DDR_ERR_ARG, "inconsistent CSR row pointers");
     std::shared_ptr<TriPlan> plan;
-    ddr_status st = get_plan(n, nnz, crow, col, lower ? 1 : 0, transpose ? 1 : 0, &plan);
+    const int unit = unit_diagonal ? 1 : 0;
+    ddr_status st = get_plan(n, nnz, crow, col, lower ? 1 : 0, transpose ? 1 : 0, unit, &plan);
     if (st) return st;
     TriPlan& P = *plan;
     std::lock_guard<std::mutex> lk(P.mu);
@@ -213,8 +219,9 @@ extern "C" ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow,
     hipStream_t s = static_cast<hipStream_t>(stream);
     DDR_HIP(hipMemsetAsync(d_flag, 0, sizeof(unsigned), s));
     hipLaunchKernelGGL(tri_solve_kernel, dim3(1), dim3(1024), 0, s, n, d_lvl, P.nlvl, d_order, d_eptr, d_edep, d_eval,
-                       d_diag, values, b, d_y, x, d_flag);
+                       d_diag, values, b, d_y, x, d_flag, unit);
     DDR_HIP(hipGetLastError());
+    if (unit) return DDR_OK;  // nothing to check: no host round trip
     // the singular check is the error contract of the reference solver (utils.py:598-600): one
     // 4-byte read back per solve
     unsigned flag = 0;
@@ -225,6 +232,12 @@ extern "C" ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow,
   } catch (...) {
     return fail(DDR_ERR_ARG, "internal error in ddr_tri_solve");
   }
+}
+
+extern "C" ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
+                                    const float* values, const float* b, float* x, int32_t lower,
+                                    int32_t transpose, void* stream) {
+  return ddr_tri_solve_ex(n, nnz, crow, col, values, b, x, lower, transpose, 0, stream);
 }
 
 extern "C" ddr_status ddr_tri_grad_values(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,

@@ -94,6 +94,16 @@ def _unit_values(vals) -> np.ndarray:
     return keep
 
 
+def pool_trim() -> int:
+    """Release the library's idle pooled blocks (device blocks of device-built / stream-ordered graphs,
+    pinned staging): the pools keep freed blocks for reuse (hipFree / hipHostFree synchronise with the
+    device), so a trainer whose batch sizes change can return the peak to HIP (``ddr_pool_trim``).
+    Returns the bytes released."""
+    freed = C.c_int64()
+    _lib.check(_lib.load().ddr_pool_trim(C.byref(freed)))
+    return int(freed.value)
+
+
 class RiverGraph:
     """Validated, partitioned river network uploaded to the current HIP device.
 
@@ -101,7 +111,10 @@ class RiverGraph:
     (``ddr_graph_build``), or ``host_only=True`` for a build that touches no device -- or device
     tensors, or ``on_device=True``: then the whole build runs on the device (``ddr_graph_build_device``,
     north star (1)) on ``stream`` (default: the current stream) and the schedule never leaves it.  Both
-    builders emit the same schedule for the same COO (:meth:`fingerprint`)."""
+    builders emit the same schedule for the same COO (:meth:`fingerprint`).  A host build given a
+    ``stream`` uploads its schedule stream-ordered on it (``ddr_graph_build_async``: one pinned staging
+    block, one pooled device block, no device-wide synchronisation); its memory is then released
+    stream-ordered too (:meth:`close`)."""
 
     def __init__(self, n: int, rows, cols, *, max_block_reaches: int = 0, target_blocks: int = 0,
                  max_resident: int = 0, steps_hint: int = 0, host_only: bool = False, device=None,
@@ -120,6 +133,7 @@ class RiverGraph:
         self.host_only = host_only
         self.device = None
         self.device_built = on_device
+        self._stream_ordered = on_device
         if on_device:
             if dev_tensor:
                 dev = rows.device
@@ -148,8 +162,13 @@ class RiverGraph:
                 dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
                 self.device = dev
                 with torch.cuda.device(dev):
-                    _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data,
-                                                   C.byref(opts), C.byref(handle)))
+                    if stream is not None:
+                        _lib.check(lib.ddr_graph_build_async(int(n), len(rows), rows.ctypes.data, cols.ctypes.data,
+                                                             C.byref(opts), stream.cuda_stream, C.byref(handle)))
+                        self._stream_ordered = True
+                    else:
+                        _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data,
+                                                       C.byref(opts), C.byref(handle)))
             else:
                 _lib.check(lib.ddr_graph_build(int(n), len(rows), rows.ctypes.data, cols.ctypes.data, C.byref(opts),
                                                C.byref(handle)))
@@ -167,6 +186,7 @@ class RiverGraph:
         g.host_only = False
         g.device = device
         g.device_built = device_built
+        g._stream_ordered = device_built
         info = _lib.GraphInfo()
         _lib.check(_lib.load().ddr_graph_get_info(handle, C.byref(info)))
         g.info = GraphInfo(**{f: int(getattr(info, f)) for f, _ in _lib.GraphInfo._fields_})
@@ -185,19 +205,24 @@ class RiverGraph:
         n, r, c = adjacency_to_coo(adj)
         return cls(n, r, c, **kw)
 
-    def upload(self, device=None) -> "RiverGraph":
+    def upload(self, device=None, stream=None) -> "RiverGraph":
         """Upload a host-only build to ``device`` (default: the current HIP device); returns self.
 
         The host build (``host_only=True``) touches no device and releases the GIL inside the C
         call, so it can run on a worker thread while the device routes another batch
-        (:class:`GraphPrefetcher`); only this step is on the device's thread."""
+        (:class:`GraphPrefetcher`); only this step is on the device's thread.  With ``stream`` the
+        upload is stream-ordered on it (``ddr_graph_upload_async``: no host wait)."""
         if not self.host_only:
             return self
         import torch
 
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         with torch.cuda.device(dev):
-            _lib.check(_lib.load().ddr_graph_upload(self._handle))
+            if stream is not None:
+                _lib.check(_lib.load().ddr_graph_upload_async(self._handle, stream.cuda_stream))
+                self._stream_ordered = True
+            else:
+                _lib.check(_lib.load().ddr_graph_upload(self._handle))
         self.device = dev
         self.host_only = False
         return self
@@ -270,7 +295,7 @@ class RiverGraph:
 
     def close(self) -> None:
         if self._handle is not None and self._handle.value:
-            if self.device_built:
+            if getattr(self, "_stream_ordered", False):
                 # stream-ordered release after the work queued on the current stream (the routing launches
                 # that used this graph): no device-wide synchronisation per training batch
                 import torch

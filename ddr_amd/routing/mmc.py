@@ -90,23 +90,45 @@ def _apply_data_override(derived: torch.Tensor, data: torch.Tensor | None) -> to
 
 
 class MuskingumCunge:
-    """Muskingum-Cunge routing engine (mmc.py:171-630) on the fused HIP kernels."""
+    """Muskingum-Cunge routing engine (mmc.py:171-630) on the fused HIP kernels.
+
+    The cold start's hot-start state (mmc.py:330-342) is materialised lazily: ``forward`` runs it as
+    step 0 of its own fused launch (the kernel's t = 0 branch: the same accumulation, the same bits), so a
+    training step makes one routing launch, not a separate T = 1 launch first; reading ``_discharge_t``
+    before ``forward`` (tests, BMI ``initialize``) runs that launch then, with the same result.
+    """
+
+    @property
+    def _discharge_t(self) -> torch.Tensor | None:
+        if self._hot_pending is not None:
+            mapper, qp = self._hot_pending  # (the q' of the setup_inputs that made the cold start)
+            self._hot_pending = None
+            self._state = compute_hotstart_discharge(qp[0].to(self.device), mapper, self.discharge_lb, self.device)
+        return self._state
+
+    @_discharge_t.setter
+    def _discharge_t(self, value: torch.Tensor | None) -> None:
+        self._hot_pending = None
+        self._state = value
 
     def __init__(self, cfg: Any, device: str | torch.device = "cpu") -> None:
         self.cfg = cfg
         self.device = device
-        # forward coefficient arithmetic of the fused kernel, the same default as ops.route ``math``:
-        # "exact" (default: the reference's operation order, IEEE division, correctly rounded pow --
-        # bit-identical to the oracle), "faithful" (the same order and divisions, pows in fp32
-        # faithful-class arithmetic, the accuracy class of the reference's own Sleef powf; what
-        # bench.py times) or "fast"; cfg.params.routing_math or DDR_ROUTING_MATH select another
-        self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "exact")
+        # forward coefficient arithmetic of the fused kernel: "faithful" (default: the reference's
+        # operation order and IEEE divisions, the three pows in fp32 faithful-class arithmetic -- at most
+        # 1 ulp, the accuracy class of the reference's own Sleef powf; <= 4.6e-7 from the reference's
+        # goldens, tests/test_gpu_fastmath.py; what bench.py times), "exact" (correctly rounded pow:
+        # bit-identical to the oracle, ops.route's default) or "fast"; cfg.params.routing_math or
+        # DDR_ROUTING_MATH select another
+        self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "faithful")
         if self.math not in ("exact", "faithful", "fast"):
             raise ValueError(f"routing_math must be 'exact', 'faithful' or 'fast', not {self.math!r}")
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None
-        self._discharge_t: torch.Tensor | None = None
+        self._hot_pending: tuple | None = None  # (mapper, q') of a cold start whose hot start has not run yet
+        self._state: torch.Tensor | None = None
+        self._discharge_t = None
         self.network: torch.Tensor | None = None
         self.parameter_bounds = self.cfg.params.parameter_ranges
         self.p_spatial = torch.tensor(self.cfg.params.defaults["p_spatial"], device=self.device)
@@ -191,7 +213,7 @@ class MuskingumCunge:
 
     def _init_discharge_state(self, carry_state: bool) -> None:
         """Cold start via topological accumulation, or carry (mmc.py:330-342)."""
-        if carry_state and self._discharge_t is not None:
+        if carry_state and (self._state is not None or self._hot_pending is not None):
             return
         assert self.q_prime is not None, "q_prime must be set before initializing discharge state"
         # mmc.py:335 -- one reduction pass over q' (a NaN makes the sum NaN); the elementwise check
@@ -199,13 +221,18 @@ class MuskingumCunge:
         if bool(torch.isnan(self.q_prime.sum())):
             assert ~torch.any(torch.isnan(self.q_prime)), "q_prime has NaN flows"
         mapper, _, _ = self.create_pattern_mapper()
-        self._discharge_t = compute_hotstart_discharge(self.q_prime[0].to(self.device), mapper, self.discharge_lb,
-                                                       self.device)
+        if getattr(mapper, "graph", None) is not None:
+            self._state = None
+            self._hot_pending = (mapper, self.q_prime)  # forward's launch runs it, or the first read of _discharge_t
+        else:
+            self._discharge_t = compute_hotstart_discharge(self.q_prime[0].to(self.device), mapper,
+                                                           self.discharge_lb, self.device)
 
     def _precompute_scatter_indices(self) -> None:
         """Gauge mode when len(outflow_idx) != N (mmc.py:344-363)."""
-        assert self._discharge_t is not None, "discharge state must be initialized before scatter indices"
-        n = len(self._discharge_t)
+        assert self._state is not None or self._hot_pending is not None, \
+            "discharge state must be initialized before scatter indices"
+        n = self.q_prime.shape[1]
         if self.output_indices is not None and len(self.output_indices) != n:
             self._gauges = GaugeMap.build(self.output_indices, n, self.device)
             self._flat_indices = self._gauges.index
@@ -228,16 +255,19 @@ class MuskingumCunge:
         """Fused forward over the whole window (mmc.py:365-443)."""
         if self.routing_dataclass is None:
             raise ValueError("routing_dataclass not set. Call setup_inputs() first.")
-        if self.q_prime is None or self._discharge_t is None:
+        if self.q_prime is None or (self._state is None and self._hot_pending is None):
             raise ValueError("Streamflow not set. Call setup_inputs() first.")
         if self._graph is None:
             raise RuntimeError("MuskingumCunge.forward runs on the HIP device only (no CPU fallback); "
                                "construct it with a cuda device")
         qp = self.q_prime.to(torch.float32)
+        # a pending cold start of this q': the launch's own step 0 is the hot start (mmc.py:25-66, 385, 412)
+        own = self._hot_pending is not None and self._hot_pending[1] is self.q_prime
+        q0 = None if own else self._discharge_t
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
-                                       self.slope, self.x_storage, q0=self._discharge_t, gauges=self._gauges,
+                                       self.slope, self.x_storage, q0=q0, gauges=self._gauges,
                                        consts=self._consts(), math=self.math)
-        self._discharge_t = q_last
+        self._discharge_t = q_last  # (also clears the pending cold start)
         if qp.shape[0] > 1:
             self.top_width = _apply_data_override(tw, self._data_top_width)
             self.side_slope = _apply_data_override(ss, self._data_side_slope)

@@ -69,7 +69,8 @@ class dmc(torch.nn.Module):  # noqa: N801  (reference class name)
                          spatial_parameters=kwargs["spatial_parameters"],
                          carry_state=kwargs.get("carry_state", False))
         self.network, self.n, self.q_spatial, self.p_spatial = eng.network, eng.n, eng.q_spatial, eng.p_spatial
-        self._discharge_t = eng._discharge_t
+        # (the reference mirrors _discharge_t here too, overwritten below before the caller can see it: not
+        # read here, so a cold start's hot start runs inside forward's launch)
         output = eng.forward()
         self.top_width, self.side_slope = eng.top_width, eng.side_slope
         self._discharge_t = eng._discharge_t

@@ -111,7 +111,7 @@ def _compute_row_indices_gpu(crow_indices: torch.Tensor, nnz: int) -> torch.Tens
     return torch.repeat_interleave(torch.arange(len(counts), device=crow_indices.device, dtype=torch.long), counts)
 
 
-def _tri_solve(A_values, crow_host, col_host, rhs, lower: bool, transpose: bool) -> torch.Tensor:
+def _tri_solve(A_values, crow_host, col_host, rhs, lower: bool, transpose: bool, unit: bool = False) -> torch.Tensor:
     if not rhs.is_cuda:
         raise RuntimeError("triangular_sparse_solve runs on the HIP device only (no CPU fallback); use cuda tensors")
     n = crow_host.numel() - 1
@@ -121,8 +121,8 @@ def _tri_solve(A_values, crow_host, col_host, rhs, lower: bool, transpose: bool)
     crow = np.ascontiguousarray(crow_host.numpy().astype(np.int64))
     col = np.ascontiguousarray(col_host.numpy().astype(np.int64))
     lib = _lib.load()
-    _lib.check(lib.ddr_tri_solve(n, len(col), crow.ctypes.data, col.ctypes.data, vals.data_ptr(), b.data_ptr(),
-                                 x.data_ptr(), int(lower), int(transpose), _lib.stream_ptr(rhs.device)))
+    _lib.check(lib.ddr_tri_solve_ex(n, len(col), crow.ctypes.data, col.ctypes.data, vals.data_ptr(), b.data_ptr(),
+                                    x.data_ptr(), int(lower), int(transpose), int(unit), _lib.stream_ptr(rhs.device)))
     return x.to(rhs.dtype)
 
 
@@ -130,29 +130,31 @@ class TriangularSparseSolver(torch.autograd.Function):
     """Sparse triangular solve A x = b with gradients for A's values and b (utils.py:515-692).
 
     Forward and the transposed backward solve accumulate in fp64 from fp32 values (the reference's
-    SciPy semantics, utils.py:587-600, 188-242) on the HIP device.
+    SciPy semantics, utils.py:587-600, 188-242) on the HIP device.  ``unit_diagonal`` as SciPy / CuPy
+    (utils.py:596, 611; backward 239, 307): every diagonal entry is taken as 1 and never read, in both
+    directions; the value gradient still covers every stored entry (utils.py:321-389).
     """
 
     @staticmethod
     def forward(ctx, A_values, crow_indices, col_indices, b, lower, unit_diagonal, device):
-        if unit_diagonal:
-            raise NotImplementedError("unit_diagonal=True is not used by the routing path")
         crow_h = crow_indices.detach().cpu().to(torch.int64)
         col_h = col_indices.detach().cpu().to(torch.int64)
         try:
-            x = _tri_solve(A_values, crow_h, col_h, b, bool(lower), False)
+            x = _tri_solve(A_values, crow_h, col_h, b, bool(lower), False, bool(unit_diagonal))
         except _lib.DDRError as e:
             log.error(f"HIP triangular sparse solve failed: {e}")
             raise ValueError(f"HIP triangular sparse solver failed: {e}") from e
         ctx.save_for_backward(A_values, crow_indices, col_indices, x, b)
         ctx.crow_h, ctx.col_h = crow_h, col_h
         ctx.lower = lower
+        ctx.unit_diagonal = bool(unit_diagonal)
         return x
 
     @staticmethod
     def backward(ctx, grad_output):
         A_values, crow_indices, col_indices, x, b = ctx.saved_tensors
-        gradb = _tri_solve(A_values, ctx.crow_h, ctx.col_h, grad_output.contiguous(), bool(ctx.lower), True)
+        gradb = _tri_solve(A_values, ctx.crow_h, ctx.col_h, grad_output.contiguous(), bool(ctx.lower), True,
+                           ctx.unit_diagonal)
         gradA = None
         if A_values.requires_grad:
             gradA = torch.empty(A_values.shape, device=A_values.device, dtype=torch.float32)

@@ -93,6 +93,12 @@ typedef struct {
  * Synchronous (the only host-synchronising call besides ddr_graph_status). */
 ddr_status ddr_graph_build(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
                            const ddr_build_opts* opts, ddr_graph** out);
+/* The same host build with the schedule upload stream-ordered on `stream` (SURVEY §8(b)'s
+ * ddr_graph_build(..., hipStream_t, ...)): one pinned staging block, one pooled device block, one copy on
+ * `stream`; routing launches on any stream wait for it (no hipMalloc / device-wide synchronisation).
+ * The host part (validation, partition) is synchronous and returns the counts, as ddr_graph_build. */
+ddr_status ddr_graph_build_async(int64_t n, int64_t e, const int32_t* rows, const int32_t* cols,
+                                 const ddr_build_opts* opts, void* stream, ddr_graph** out);
 /* The same build from a COO in DEVICE memory (rows / cols: int32 device pointers on the current HIP
  * device), computed on the device on `stream` (north star (1)): validation, canonical CSR, distance
  * to outlet, basins, the stem-preserving split and the whole per-workgroup schedule are device
@@ -150,13 +156,20 @@ ddr_status ddr_collate_gauges_device(int64_t n_conus, int64_t n_gauges, int64_t 
  * data-loader worker preparing the next training batch, merit.py:197-223) while the device routes
  * the current one; only this step touches the device.  Synchronous. */
 ddr_status ddr_graph_upload(ddr_graph* g);
+/* ddr_graph_upload stream-ordered on `stream` (as ddr_graph_build_async): returns without a host wait. */
+ddr_status ddr_graph_upload_async(ddr_graph* g, void* stream);
 /* Any graph size builds: workgroups take ticket-ordered logical blocks, so a schedule with more
- * blocks than co-resident workgroups still completes (ddr_graph_info.generations > 1). */
+ * blocks than co-resident workgroups still completes (ddr_graph_info.generations > 1).
+ * ddr_graph_destroy is synchronous: a graph with pooled (stream-ordered) memory waits for the device. */
 ddr_status ddr_graph_destroy(ddr_graph* g);
 /* Destroy a graph whose last use is queued on `stream`: a device-built graph's memory is released
  * stream-ordered (no device-wide synchronisation -- the per-batch graphs of a training loop); a
  * host-built one's as ddr_graph_destroy. */
 ddr_status ddr_graph_destroy_async(ddr_graph* g, void* stream);
+/* Release every idle block of the library's memory pools (device blocks of device-built graphs and
+ * async uploads, pinned staging blocks) whose last user's queued work has finished; *freed_bytes
+ * (may be NULL) receives the bytes returned to HIP.  Blocks handed out or still in use stay. */
+ddr_status ddr_pool_trim(int64_t* freed_bytes);
 ddr_status ddr_graph_get_info(const ddr_graph* g, ddr_graph_info* info);
 /* Canonical CSR of the adjacency into host buffers: crow (n+1), col (nnz), int64. */
 ddr_status ddr_graph_csr(const ddr_graph* g, int64_t* crow, int64_t* col);
@@ -377,6 +390,12 @@ ddr_status ddr_set_debug_flags(int32_t flags);
 ddr_status ddr_tri_solve(int64_t n, int64_t nnz, const int64_t* crow_host, const int64_t* col_host,
                          const float* values, const float* b, float* x, int32_t lower,
                          int32_t transpose, void* stream);
+/* ddr_tri_solve with SciPy's / CuPy's unit_diagonal (routing/utils.py:596, 611 forward; 239, 307
+ * backward): unit_diagonal != 0 takes every diagonal entry as 1 without reading it (a missing one
+ * included) and skips the diag^-1 scaling and the singular check (no host round trip). */
+ddr_status ddr_tri_solve_ex(int64_t n, int64_t nnz, const int64_t* crow_host, const int64_t* col_host,
+                            const float* values, const float* b, float* x, int32_t lower,
+                            int32_t transpose, int32_t unit_diagonal, void* stream);
 /* gradA[k] = -gradb[row(k)] * x[col(k)] for CSR (device int64 crow/col). */
 ddr_status ddr_tri_grad_values(int64_t n, int64_t nnz, const int64_t* crow, const int64_t* col,
                                const float* gradb, const float* x, float* grad_values, void* stream);

@@ -24,7 +24,8 @@ def case():
     return net, at, u, qp, W
 
 
-def route_once(g, net, at, u, qp, W, math, dev):
+def route_forward(g, net, at, u, qp, math, dev):
+    """Forward only: (runoff, the unit parameters it depends on, last-step Q); backward later."""
     import torch
 
     from ddr_amd.ops import route
@@ -33,11 +34,27 @@ def route_once(g, net, at, u, qp, W, math, dev):
     un = {k: tt(u[k]).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial")}
     n = un["n"] * 0.2 + 0.02
     p = torch.exp(un["p_spatial"] * 5.0)
-    runoff, _, _, _ = route(g, tt(qp), n, un["q_spatial"], p, tt(at.length), tt(np.maximum(at.slope, 1e-3)), tt(at.x),
-                            math=math)
-    (runoff * tt(W)).sum().backward()
+    runoff, q_last, _, _ = route(g, tt(qp), n, un["q_spatial"], p, tt(at.length), tt(np.maximum(at.slope, 1e-3)),
+                                 tt(at.x), math=math)
+    return runoff, un, q_last
+
+
+def route_backward(runoff, un, W, dev):
+    import torch
+
+    (runoff * torch.from_numpy(W).to(dev)).sum().backward()
     torch.cuda.synchronize()
     return {"runoff": runoff.detach().cpu().numpy(), **{f"g_{k}": v.grad.cpu().numpy() for k, v in un.items()}}
+
+
+def route_once(g, net, at, u, qp, W, math, dev):
+    runoff, un, _ = route_forward(g, net, at, u, qp, math, dev)
+    return route_backward(runoff, un, W, dev)
+
+
+def second_inputs(qp):
+    """A second batch of lateral inflow (the interleaved forward / forward / backward / backward case)."""
+    return (qp * np.float32(1.7) + np.float32(0.05)).astype(np.float32)
 
 
 def main():
@@ -68,9 +85,32 @@ def main():
     sb = SplitBasin(g, br, rank, world, T, exchange)
     res = [route_once(g, net, at, u, qp, W, math, dev) for _ in range(2)]  # two launches: epochs advance
     check_status()
+    # forward A, forward B, backward A, backward B: forward B rewrites the shared receive rows before
+    # backward A runs (each backward must read its own forward's cross-rank x)
+    ra, ua, qa = route_forward(g, net, at, u, qp, math, dev)
+    rb, ub, _ = route_forward(g, net, at, u, second_inputs(qp), math, dev)
+    res.append(route_backward(ra, ua, W, dev))
+    res.append(route_backward(rb, ub, W, dev))
+    check_status()
+    # outputs of reaches another rank routes are marked, never stale memory
+    notown = np.setdiff1d(np.arange(net.n), sb.owned_reaches)
+    extra = {"nan_col0": bool(np.isnan(res[2]["runoff"][notown, 0]).all()),
+             "nan_qlast": bool(torch.isnan(qa[torch.from_numpy(notown).to(dev)]).all().item()),
+             "own_finite": bool(np.isfinite(res[2]["runoff"][sb.owned_reaches]).all())}
+    from ddr_amd.ops import GaugeMap, route
+
+    try:  # gauge mode on a split graph is refused
+        gz = GaugeMap.build([np.array([net.n - 1])], net.n, dev)
+        z = torch.ones(net.n, device=dev)
+        route(g, torch.from_numpy(qp).to(dev), z * 0.05, z * 0.5, z * 20, z * 1000, z * 0.01, z * 0.3, gauges=gz,
+              math=math)
+        extra["gauge_refused"] = False
+    except Exception as e:  # noqa: BLE001
+        extra["gauge_refused"] = "split basin" in str(e)
+    dist.barrier()
     dist.barrier()
     sb.close()
-    np.savez(out, owned=sb.owned_reaches, n_x=sb.n_x, kind=sb.kind, fp=np.uint64(g.fingerprint()),
+    np.savez(out, owned=sb.owned_reaches, n_x=sb.n_x, kind=sb.kind, fp=np.uint64(g.fingerprint()), **extra,
              **{f"{i}_{k}": v for i, r in enumerate(res) for k, v in r.items()})
     dist.destroy_process_group()
 

@@ -203,3 +203,37 @@ def test_pending_builds_begun_ahead_match_host_builds(cuda):
     with pytest.raises(_lib.DDRError) as e:
         bad.finish()
     assert e.value.code == _lib.DDR_ERR_NOT_DENDRITIC
+
+
+def test_stream_ordered_host_build_and_pool_trim(cuda):
+    """ddr_graph_build_async / ddr_graph_upload_async (the build's upload on a stream) give
+    the host build's schedule, route like it, release stream-ordered; ddr_pool_trim returns idle pool
+    blocks and later builds still work."""
+    from ddr_amd.graph import pool_trim
+    from ddr_amd.ops import route
+
+    net = synthetic.forest(synthetic.loguniform_sizes(40, 20, 2000, 9), seed=9, single_inflow=0.3)
+    kw = {"max_block_reaches": 400, "target_blocks": 1 << 20}
+    h = RiverGraph(net.n, net.rows, net.cols, **kw)
+    st = torch.cuda.Stream()
+    a = RiverGraph(net.n, net.rows, net.cols, stream=st, **kw)
+    ho = RiverGraph(net.n, net.rows, net.cols, host_only=True, **kw).upload(stream=st)
+    torch.cuda.current_stream().wait_stream(st)
+    assert h.fingerprint() == a.fingerprint() == ho.fingerprint()
+    T = 48
+    at = synthetic.reach_attributes(net.n, 3)
+    qp = torch.from_numpy(synthetic.lateral_inflow(net.n, T, 3)).to(cuda)
+    tt = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(cuda, torch.float32)  # noqa: E731
+    z = torch.full((net.n,), 0.5, device=cuda)
+    args = (qp, z * 0.1, z, z * 20, tt(at.length), tt(np.maximum(at.slope, 1e-3)), tt(at.x))
+    ref = route(h, *args)[0]
+    for g in (a, ho):
+        assert torch.equal(route(g, *args)[0], ref)
+    for g in (a, ho, h):
+        g.close()
+    torch.cuda.synchronize()
+    assert pool_trim() >= 0
+    assert pool_trim() == 0  # nothing idle is left after a trim
+    b = RiverGraph(net.n, net.rows, net.cols, stream=torch.cuda.current_stream(), **kw)
+    assert torch.equal(route(b, *args)[0], ref)
+    b.close()

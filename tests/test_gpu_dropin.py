@@ -194,6 +194,40 @@ def test_triangular_solve_known_answer(cuda):
                                 torch.ones(n, device=cuda), True, False, cuda)
 
 
+def test_triangular_solve_unit_diagonal_matches_scipy(cuda):
+    """unit_diagonal=True (routing/utils.py:596, 611; backward 239, 307): SciPy's semantics -- the stored
+    diagonal is ignored (one row has none), no diag^-1 scaling; gradients through the transposed solve."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import spsolve_triangular
+
+    rng = np.random.default_rng(4)
+    n = 300
+    dense = np.tril(rng.uniform(-0.4, 0.4, (n, n)) * (rng.uniform(0, 1, (n, n)) < 0.02), -1)
+    np.fill_diagonal(dense, rng.uniform(2.0, 3.0, n))  # never read
+    dense[7, 7] = 0.0  # a row without a stored diagonal entry
+    a = sp.csr_matrix(dense.astype(np.float32))
+    a.sort_indices()
+    b = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    g = rng.uniform(-1, 1, n).astype(np.float32)
+    a64 = sp.csr_matrix((a.data.astype(np.float64), a.indices, a.indptr), shape=(n, n))
+    x_ref = spsolve_triangular(a64, b.astype(np.float64), lower=True, unit_diagonal=True).astype(np.float32)
+    gb_ref = spsolve_triangular(a64.T, g.astype(np.float64), lower=False, unit_diagonal=True).astype(np.float32)
+    A = torch.from_numpy(a.data).to(cuda).requires_grad_(True)
+    bt = torch.from_numpy(b).to(cuda).requires_grad_(True)
+    crow, col = torch.from_numpy(a.indptr.astype(np.int64)), torch.from_numpy(a.indices.astype(np.int64))
+    x = triangular_sparse_solve(A, crow, col, bt, True, True, cuda)
+    assert maxrel(x.detach().cpu().numpy(), x_ref) <= 1e-6
+    (x * torch.from_numpy(g).to(cuda)).sum().backward()
+    assert maxrel(bt.grad.cpu().numpy(), gb_ref) <= 1e-6
+    rows = np.repeat(np.arange(n), np.diff(a.indptr))
+    ga_ref = -gb_ref[rows] * x_ref[a.indices]  # _compute_A_gradients, every stored entry
+    np.testing.assert_allclose(A.grad.cpu().numpy(), ga_ref, rtol=1e-5, atol=1e-7)
+    # a zero stored diagonal is not an error with unit_diagonal (SciPy setdiag(1))
+    z = triangular_sparse_solve(torch.zeros(5, device=cuda), torch.arange(6), torch.arange(5),
+                                torch.arange(1.0, 6.0, device=cuda), True, True, cuda)
+    np.testing.assert_array_equal(z.cpu().numpy(), np.arange(1.0, 6.0))
+
+
 def test_triangular_solve_routing_matrix(cuda):
     """A = I - diag(c1) N from the mapper path equals the fp64 oracle sweep."""
     from oracle import mc_oracle as O

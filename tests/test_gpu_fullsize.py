@@ -181,6 +181,56 @@ def test_c5_giant_basin_oracle_and_partition_invariance(c5):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("t0", [2000, 5000, 8700])
+def test_c5_giant_basin_windows_across_the_water_year(c5, t0):
+    """The 281k-reach, 2215-deep basin pinned against the oracle across the whole year, not only its first
+    hours: the kernel's own state at hour t0 of the full 8760-h run (runoff[:, t0] = Q(t0)) is carried into
+    a 36-h window (the reference's carry_state, mmc.py:330-333; scripts/router.py:160-166) and routed
+    (1) by the kernel from that state, which must reproduce the full run's hours t0 .. t0 + 35 bit for bit;
+    (2) by the fp32 oracle from the same state (max-rel <= 1e-6, bitwise expected); and (3) the window's
+    parameter gradients: the fp64 kernel equals the fp64 oracle adjoint (norm-rel <= 1e-10, the algorithm
+    is exact), and the fp32 kernel is within the fp32 rounding that accumulates along this chain in any
+    fp32 adjoint (the reference's own fp32 gradients on this basin are 2.6e-3 / 7.9e-3 / 4.3e-3 from the
+    fp64 adjoint, tests/golden/deep.npz; bar 5e-3 / 1e-2 / 5e-3)."""
+    L = 36
+    members, _ = _basins_by_blocks(c5)
+    ids = np.sort(members[int(np.argmax([len(m) for m in members]))])
+    assert len(ids) > 250_000
+    ns, rs, cs = c5.basin(ids)
+    sel = torch.from_numpy(ids).to(c5.dev)
+    full = c5.out["runoff"][sel]
+    q0 = full[:, t0].contiguous()
+    qp = c5.qprime[t0:t0 + L][:, sel].contiguous()
+    gen = torch.Generator(device=c5.dev).manual_seed(t0)
+    W = torch.rand((len(ids), L), device=c5.dev, dtype=torch.float32, generator=gen)
+    at = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a[ids])).to(c5.dev, dt)  # noqa: E731
+    res = {}
+    for dt, gkw in ((torch.float32, {}), (torch.float64, {"max_block_reaches": 1024})):
+        g = RiverGraph(ns, rs, cs, steps_hint=L, **gkw)
+        n, q, p = (at(a, dt).requires_grad_(True) for a in (c5.n, c5.q, c5.p))
+        runoff, _, _, _ = route(g, qp.to(dt), n, q, p, at(c5.length, dt), at(c5.slope, dt), at(c5.x, dt),
+                                q0=q0.to(dt), consts=RouteConsts())
+        runoff.backward(W.to(dt))
+        torch.cuda.synchronize()
+        res[dt] = {"runoff": runoff.detach().cpu().numpy(),
+                   **{k: v.grad.cpu().numpy().astype(np.float64) for k, v in (("n", n), ("q_spatial", q), ("p_spatial", p))}}
+        del g, runoff, n, q, p
+    got = res[torch.float32]["runoff"]
+    np.testing.assert_array_equal(got, full[:, t0:t0 + L].cpu().numpy())  # the full run, continued bit for bit
+    net = O.Network.from_coo(ns, rs, cs)
+    r = O.Reaches(c5.n[ids], c5.q[ids], c5.p[ids], c5.length[ids], c5.slope[ids], c5.x[ids])
+    qn, q0n, Wn = qp.cpu().numpy(), q0.cpu().numpy(), W.cpu().numpy()
+    ref = O.route(net, r, qn, O.Bounds(), q0=q0n, dtype=np.float32)
+    assert maxrel(got, ref["runoff"]) <= 1e-6
+    r64 = O.route(net, r, qn, O.Bounds(), q0=q0n, dtype=np.float64)
+    assert maxrel(res[torch.float64]["runoff"], r64["runoff"]) <= 1e-12
+    gref = O.route_backward(net, r, qn, r64["x"], Wn, O.Bounds(), carry=True)
+    for k, bar in (("n", 5e-3), ("q_spatial", 1e-2), ("p_spatial", 5e-3)):
+        assert normrel(res[torch.float64][k], gref[k]) <= 1e-10, k
+        assert normrel(res[torch.float32][k], gref[k]) <= bar, k
+    torch.cuda.empty_cache()
+
+
 def test_deep_basin_gradients_vs_reference(cuda):
     """Gradients along a 2215-hop chain (tests/golden/deep.npz: the reference itself on C5's 281k-reach
     basin over 24 h).  fp32 rounding accumulates along the chain in ANY fp32 adjoint: the reference's

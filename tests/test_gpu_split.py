@@ -34,6 +34,7 @@ def test_split_basin_processes_bitwise(cuda, tmp_path, math, world):
     g = RiverGraph(net.n, net.rows, net.cols, **W.GRAPH_KW)
     assert g.info.n_blocks >= 4 and g.info.n_cut > 0
     ref = W.route_once(g, net, at, u, qp, Wt, math, cuda)
+    ref_b = W.route_once(g, net, at, u, W.second_inputs(qp), Wt, math, cuda)
     port = _free_port()
     outs = [str(tmp_path / f"r{r}.npz") for r in range(world)]
     env = dict(os.environ, PYTHONUNBUFFERED="1")
@@ -55,7 +56,10 @@ def test_split_basin_processes_bitwise(cuda, tmp_path, math, world):
     owned = [d["owned"] for d in got]
     assert np.array_equal(np.sort(np.concatenate(owned)), np.arange(net.n))  # a partition of the reaches
     for d, own in zip(got, owned):
-        for i in range(2):
-            assert np.array_equal(d[f"{i}_runoff"][own], ref["runoff"][own])
+        # launches 0, 1: forward + backward each; 2, 3: forward A, forward B, backward A, backward B
+        for i, r in ((0, ref), (1, ref), (2, ref), (3, ref_b)):
+            assert np.array_equal(d[f"{i}_runoff"][own], r["runoff"][own]), i
             for k in ("g_n", "g_q_spatial", "g_p_spatial"):
-                assert np.array_equal(d[f"{i}_{k}"][own], ref[k][own]), k
+                assert np.array_equal(d[f"{i}_{k}"][own], r[k][own]), (i, k)
+        assert d["nan_col0"] and d["nan_qlast"] and d["own_finite"]
+        assert d["gauge_refused"]
