@@ -329,8 +329,8 @@ ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* ou
   }
   int64_t maxl = 0;
   for (int64_t b = 0; b < nblocks; ++b) maxl = std::max(maxl, load[b]);
-  const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4, fwd_xbuf(kr_of_load(maxl))),
-                               route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4));
+  const size_t need = std::max(route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, false, 4, kr_of_load(maxl)),
+                               route_lds_bytes(route_slot_stride((int)ms), mv, mc, mx, true, 4, kr_of_load(maxl)));
   if (P.dbg) fprintf(stderr, "[part]   slots %ld virt %ld cout %ld xl %ld lds %zu\n", (long)ms, (long)mv, (long)mc, (long)mx, need);
   // (a count failure at the capacity ceiling of the unweighted packing goes to more generations:
   // shrinking the capacity for LDS would only add blocks)

@@ -62,6 +62,12 @@ __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_sl
 #define DDR_FWD_DBL 1
 #endif
 __host__ __device__ constexpr int fwd_xbuf(int kr) { return (DDR_FWD_DBL && kr <= 2) ? 2 : 1; }
+// The backward's three slot arrays (c1 gb, c2 gb, published x) likewise: each tick reads the values its
+// neighbours wrote the tick before and writes the next tick's, one barrier per tick (KR <= 2)
+#ifndef DDR_BWD_DBL
+#define DDR_BWD_DBL 1
+#endif
+__host__ __device__ constexpr int bwd_xbuf(int kr) { return (DDR_BWD_DBL && kr <= 2) ? 2 : 1; }
 // reaches per thread of the routing kernels for a largest block of `max_load` reaches
 inline int kr_of_load(int64_t max_load) {
   int kr = 1;
@@ -71,7 +77,8 @@ inline int kr_of_load(int64_t max_load) {
 // Dynamic LDS of the routing kernels (route.hip), for `slots` = nloc + nvirt slots and `nring`
 // import rings (virtual inflows forward, cut-outs backward), reals of `rsize` bytes:
 //   forward : x slots (f64, xbuf buffers) | 6 statics (R) | ring [nvirt][kChunkFwd] f64
-//   backward: A slots (R) | B slots (R) | published x slots (R) | 6 statics (R) | ring [ncout][kChunkBwd][2] (R)
+//   backward: A slots (R) | B slots (R) | published x slots (R) (each xbuf buffers) | 6 statics (R)
+//             | ring [ncout][kChunkBwd][2] (R)
 //             | owner words
 // and then the block's confluence lists (after the math tables of fastmath.h, which occupy the first
 // kMathTabBytes)
@@ -80,8 +87,9 @@ constexpr size_t kMathTabBytes = 3072;
 // kMaxConfluenceList int32 entries per block (13-bit offsets in the packed upstream word).
 constexpr int kMaxConfluenceList = 8191;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nvirt, size_t ncout, size_t nxl, bool backward,
-                                                  size_t rsize, int xbuf = 1) {
-  const size_t base = backward ? slots * 9 * rsize : slots * (8 * (size_t)xbuf + 6 * rsize);
+                                                  size_t rsize, int kr = 4) {
+  const size_t base = backward ? slots * (3 * (size_t)bwd_xbuf(kr) + 6) * rsize
+                               : slots * (8 * (size_t)fwd_xbuf(kr) + 6 * rsize);
   const size_t ring = backward ? ncout * kChunkBwd * 2 * rsize : nvirt * kChunkFwd * 8;
   // backward: per hand-off owner thread (tid < max(nvirt, ncout)) its virtual's downstream slot and
   // its cut-out's tick offset

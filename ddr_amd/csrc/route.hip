@@ -991,11 +991,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // so a workgroup's tick costs ceil(nloc / 64) wave-slices, not KR * waves
   const int wbase = __builtin_amdgcn_readfirstlane(tid & ~63);
   const int S = a.slot_stride;
-  R* sa = reinterpret_cast<R*>(smem + kMathTabBytes);  // [S] c1_i gb_i (transposed solve, rounded to R)
-  R* sb = sa + S;                                       // [S] c2_i gb_i (adjoint of the inflow)
-  R* sx = sb + S;                                       // [S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
-  const StatTab<R> tab{sx + S};                         // [S][6]
-  R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * 9 * sizeof(R)));  // [ncout][kChunkBwd][2]
+  // kDbl (KR <= 2): each slot array is [2][S] by tick parity -- a tick reads what its neighbours wrote the
+  // tick before (the downstream's (c1 gb, c2 gb) in buffer (tb + 1) & 1, the upstream's x in buffer tb & 1)
+  // and writes its own for the next tick into the other buffers: one workgroup barrier per tick.  Else
+  // [S] each, a publish phase and a compute phase between two barriers.
+  constexpr int kXB = bwd_xbuf(KR);
+  constexpr bool kDbl = kXB == 2 && (DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR);
+  R* sa = reinterpret_cast<R*>(smem + kMathTabBytes);  // [kXB][S] c1_i gb_i (transposed solve, rounded to R)
+  R* sb = sa + kXB * S;                                 // [kXB][S] c2_i gb_i (adjoint of the inflow)
+  R* sx = sb + kXB * S;                                 // [kXB][S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
+  const StatTab<R> tab{sx + kXB * S};                   // [S][6]
+  R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * (3 * kXB + 6) * sizeof(R)));  // [ncout][kChunkBwd][2]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                                            // confluence lists
   const Consts<R> cs = consts_of<R>(a);
   const int64_t T = a.T;
@@ -1058,6 +1064,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (tid + k * BS == loc) od[k] = (od[k] & 0xFFFF0000u) | ((unsigned)(-(c + 2)) & 0xFFFFu);
   }
   if (tid == 0) sx[S - 1] = R(0);
+  if (kDbl && tid == 0) sx[2 * S - 1] = R(0);
   const bool vown = tid < B.nvirt;
   // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
   // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
@@ -1186,9 +1193,18 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       od[k] = opq(od[k]);
       up[k] = opq(up[k]);
     }
+    // kDbl: this tick publishes (into the next tick's x buffer) the values loaded last tick, and loads
+    // those it publishes next tick -- one tick further ahead than without double buffering
+    const R* sar = sa + (kDbl ? ((tb + 1) & 1) * S : 0);  // the downstream's values of the previous tick
+    const R* sbr = sb + (kDbl ? ((tb + 1) & 1) * S : 0);
+    R* saw = sa + (kDbl ? (tb & 1) * S : 0);              // this tick's (c1 gb, c2 gb)
+    R* sbw = sb + (kDbl ? (tb & 1) * S : 0);
+    const R* sxr = sx + (kDbl ? (tb & 1) * S : 0);        // x published for this tick
+    R* sxw = sx + (kDbl ? ((tb + 1) & 1) * S : 0);        // (kDbl) x published for the next tick
     if constexpr (kEarly) {
-      load_own(tau - 3, xbn, tq);                                  // x(t - 3), published next tick
-      if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);      // the virtual's value for the next tick
+      constexpr int ahead = kDbl ? 1 : 0;
+      load_own(tau - 3 - ahead, xbn, tq);                          // x(t - 3) (kDbl: x(t - 4)), published next tick
+      if (vown) vxn = load_virt((int64_t)tau - 1 - ahead - v_off - 2);  // the virtual's value for the next tick
     }
     if (B.ncout > 0 && (tb % kChunkBwd) == 0) {
       // one (cut-out, step) per thread and iteration, its (A, B) granule pair requested together; the
@@ -1219,20 +1235,20 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if (vown) {
       // export the consumer's (c1 gb, c2 gb) of step t (written last tick, when the consumer ran
       // step tau + 1 - off_c = tau - v_off) to the upstream block; publish the upstream reach's x
-      // at the consumer's current step - 1
+      // at the consumer's current step - 1 (kDbl: next step's, into the next tick's buffer)
       const int t = tau - v_off;
       if (t >= tmin && t < T) {
         const int dloc = v_dloc_of();
         if (vxi >= 0) {  // split basin: the producer block is another rank's (row from the block's table)
           double* dst = reinterpret_cast<double*>(xtv[tid] & ~uintptr_t(1)) + (int64_t)t * 2;
-          store_granule_sys(dst, (double)sa[dloc]);
-          store_granule_sys(dst + 1, (double)sb[dloc]);
+          store_granule_sys(dst, (double)sar[dloc]);
+          store_granule_sys(dst + 1, (double)sbr[dloc]);
         } else {
-          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sa[dloc]);
-          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sb[dloc]);
+          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2, (double)sar[dloc]);
+          store_granule(a.bwd_bnd + ((int64_t)v_edge * T + t) * 2 + 1, (double)sbr[dloc]);
         }
       }
-      sx[B.nloc + tid] = R(vxc);
+      sxw[B.nloc + tid] = R(vxc);
     }
     R A[KR], Bd[KR];
 #pragma unroll
@@ -1241,11 +1257,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       Bd[k] = R(0);
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
-      if (r < B.nloc) sx[r] = xbc[k];  // x(t - 2): the upstream value of the downstream reach's step t - 1
+      // x(t - 2): the upstream value of the downstream reach's step t - 1 (kDbl: next tick's, x(t - 3))
+      if (r < B.nloc) sxw[r] = xbc[k];
       const int dl = dl_of(k);
       if (dl >= 0) {
-        A[k] = sa[dl];
-        Bd[k] = sb[dl];
+        A[k] = sar[dl];
+        Bd[k] = sbr[dl];
       } else if (dl <= -2) {
         const int sidx = tb % kChunkBwd;
         A[k] = ring[((-dl - 2) * kChunkBwd + sidx) * 2];
@@ -1253,7 +1270,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     }
     phz.mark(2);  // read / publish
-    lds_barrier();
+    if constexpr (!kDbl) lds_barrier();
     phz.mark(3);  // barrier 1
     if constexpr (!kEarly) {
       load_own(tau - 3, xbn, tq);                    // x(t - 3), published next tick
@@ -1272,8 +1289,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // state at t - 1 = 0 is not clamped) and Sx(t - 1) for the next tick
       const bool c0 = !kSt && (t == 1 && carry);
       const int nup = up_n(up[k]);
-      const R x0 = sx[up_0(up[k])];
-      const R x1 = sx[up_1(up[k], xl)];
+      const R x0 = sxr[up_0(up[k])];
+      const R x1 = sxr[up_1(up[k], xl)];
       R sxv = R(0) + x0;
       sxv = sxv + x1;
       R I = R(0);
@@ -1283,7 +1300,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int* lst = xl + up_f1(up[k]);
         const int c = lst[0];
         for (int j = 2; j < c; ++j) {
-          const R xj = sx[lst[j]];
+          const R xj = sxr[lst[j]];
           sxv = sxv + xj;
           I = I + (c0 ? xj : rmax(xj, cs.qlb));
         }
@@ -1329,8 +1346,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           atomicAdd(g3p + 2, (double)pp[k]);
           pn[k] = pq[k] = pp[k] = R(0);
         }
-        sa[r] = R((double)c1 * gb64);
-        sb[r] = c2 * gb;
+        saw[r] = R((double)c1 * gb64);
+        sbw[r] = c2 * gb;
         lam[k] = ((gb * c3) + gQ) + Bd[k];
         // dL/dqc = gb c4 (b = ... + c4 qc), through qc = clamp(q' * flow_scale) (mmc.py:421-424)
         if constexpr (GS) gqs[xs_base + (int64_t)tau * B.nloc + r] = (qsv[k] >= cs.qlb) ? gb * c4 : R(0);
@@ -1340,13 +1357,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           // (already folded into gk through gmask0)
           if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = a.g_roff ? lm : lam[k] + ((xtk >= cs.qlb) ? gk : R(0));
           gqs[xs_base + (int64_t)tau * B.nloc + r] = R(0);
-          sa[r] = R(0);
-          sb[r] = R(0);
+          saw[r] = R(0);
+          sbw[r] = R(0);
         } else {
           // hot start x(0) = (I - N)^-1 q'[0] (mmc.py:25-66): its transposed solve (c1 = 1) is gb64
           gqs[xs_base + (int64_t)tau * B.nloc + r] = gb;
-          sa[r] = gb;
-          sb[r] = R(0);
+          saw[r] = gb;
+          sbw[r] = R(0);
         }
       }
       }  // wave_act
@@ -1371,7 +1388,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       xc[k] = xa[k];
-      xa[k] = r < B.nloc ? sx[r] : R(0);
+      xa[k] = r < B.nloc ? sxr[r] : R(0);
     }
   };
 
@@ -1387,26 +1404,39 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   load_own(TT - 2, xa, tid);
   load_own(TT - 3, xb, tid);
   // prologue: Sx of every reach's first step t0 = sum_j x_j(t0), where x_j(t0) is the upstream
-  // reach's x one step before its own first step (its xa; a virtual inflow's granule)
+  // reach's x one step before its own first step (its xa; a virtual inflow's granule) -- (kDbl) in buffer
+  // 1, which tick 0 then overwrites
+  R* sxp = sx + (kDbl ? S : 0);
 #pragma unroll
   for (int k = 0; k < KR; ++k)
-    if (tid + k * BS < B.nloc) sx[tid + k * BS] = xa[k];
-  if (vown) sx[B.nloc + tid] = R(load_virt((int64_t)(TT - 1) - v_off - 1));
+    if (tid + k * BS < B.nloc) sxp[tid + k * BS] = xa[k];
+  if (vown) sxp[B.nloc + tid] = R(load_virt((int64_t)(TT - 1) - v_off - 1));
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
     if (r >= B.nloc) continue;
-    R v = R(0) + sx[up_0(up[k])];
-    v = v + sx[up_1(up[k], xl)];
+    R v = R(0) + sxp[up_0(up[k])];
+    v = v + sxp[up_1(up[k], xl)];
     if (up_n(up[k]) > 2) {
       const int* lst = xl + up_f1(up[k]);
-      for (int j = 2; j < lst[0]; ++j) v = v + sx[lst[j]];
+      for (int j = 2; j < lst[0]; ++j) v = v + sxp[lst[j]];
     }
     sxn[k] = v;
   }
   __syncthreads();
   if (vown) vx = load_virt((int64_t)(TT - 1) - v_off - 2);
+  if constexpr (kDbl) {
+    // tick 0's published values (x(t0 - 2), the virtuals') go into its read buffer now; the registers
+    // then hold what tick 0 publishes for tick 1
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      if (tid + k * BS < B.nloc) sx[tid + k * BS] = xb[k];
+    if (vown) sx[B.nloc + tid] = R(vx);
+    load_own(TT - 4, xb, tid);
+    if (vown) vx = load_virt((int64_t)(TT - 2) - v_off - 2);
+    __syncthreads();
+  }
 #pragma unroll
   for (int k = 0; k < KR; ++k)
     if (tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
@@ -1706,7 +1736,7 @@ __global__ void gauge_daily_seed_kernel(int64_t G, int64_t T, int64_t t0, int64_
 template <typename R>
 size_t route_smem_bytes(const Graph* g, bool backward) {
   return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt, (size_t)g->max_cout,
-                         (size_t)g->max_xl, backward, sizeof(R), fwd_xbuf(g->kr));
+                         (size_t)g->max_xl, backward, sizeof(R), g->kr);
 }
 
 // Split basin: after the layout, each block's granule rows (tagged pointers, bit 0 = another rank's
