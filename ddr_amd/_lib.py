@@ -38,6 +38,7 @@ DDR_FWD_NO_RUNOFF = 4
 DDR_FWD_ACCUMULATE = 8
 DDR_FWD_FAST_MATH = 16
 DDR_FWD_FAITHFUL_MATH = 32
+DDR_FWD_CHECK_QPRIME = 64
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 DDR_DEBUG_NO_STEADY = 2
@@ -90,6 +91,7 @@ _SIGS = {
     "ddr_graph_upload_async": (C.c_int, [_P, _P]),
     "ddr_graph_build_async": (C.c_int, [_I64, _I64, _P, _P, C.POINTER(BuildOpts), _P, C.POINTER(C.c_void_p)]),
     "ddr_pool_trim": (C.c_int, [C.POINTER(C.c_int64)]),
+    "ddr_qprime_nan_wait": (C.c_int, [C.POINTER(C.c_int32)]),
     "ddr_collate_gauges": (C.c_int, [_I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "ddr_collate_gauges_device": (C.c_int, [_I64, _I64, _I64, _P, _P, _P, _P, _I64, C.POINTER(C.c_int64), _P, _P,
                                             C.POINTER(C.c_int64), _P, _P, _P, _P, _I64, _P, _P]),

@@ -126,6 +126,31 @@ struct PendingStatus {
   }
 } g_pending;
 
+// DDR_FWD_CHECK_QPRIME: per host thread, the NaN word of its last checked forward, copied to pinned memory
+// behind the q' gather, and the event after that copy (ddr_qprime_nan_wait waits for the gather only)
+struct NanCheck {
+  unsigned* host = nullptr;
+  hipEvent_t ev = nullptr;
+  bool armed = false;
+};
+thread_local NanCheck t_nan;
+
+hipError_t nan_check_mark(const void* status, hipStream_t s) {
+  if (!t_nan.host) {
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t_nan.host), 16, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+  }
+  if (!t_nan.ev) {
+    hipError_t e = hipEventCreateWithFlags(&t_nan.ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipMemcpyAsync(t_nan.host, static_cast<const unsigned*>(status) + kStatusNaN, sizeof(unsigned),
+                                hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  t_nan.armed = true;
+  return hipEventRecord(t_nan.ev, s);
+}
+
 hipError_t timing_mark(int which, int edge, hipStream_t s) {
   if (!g_timing.on) return hipSuccess;
   hipEvent_t& e = g_timing.ev[which][edge];
@@ -274,6 +299,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   a.qs = x_save + (g->n * T + g->sum_dn);
   if ((st = split_prepare(g, a, T, 0, s))) return st;
   DDR_HIP(launch_gather_qprime<R>(g, a, s));
+  if (flags & DDR_FWD_CHECK_QPRIME) DDR_HIP(nan_check_mark(status, s));
   DDR_HIP(timing_mark(0, 0, s));
   DDR_HIP(launch_route<R>(g, a, false, s));
   DDR_HIP(timing_mark(0, 1, s));
@@ -585,6 +611,17 @@ ddr_status ddr_graph_destroy(ddr_graph* g) {
     // stream, which does not order PyTorch's non-blocking streams)
     if (gr && (gr->device_built || !gr->async_allocations.empty())) DDR_HIP(hipDeviceSynchronize());
     destroy_graph(gr);
+    return DDR_OK;
+  })
+}
+
+ddr_status ddr_qprime_nan_wait(int32_t* has_nan) {
+  DDR_GUARD({
+    if (!has_nan) return fail(DDR_ERR_ARG, "null has_nan");
+    if (!t_nan.armed) return fail(DDR_ERR_ARG, "no DDR_FWD_CHECK_QPRIME forward on this thread");
+    DDR_HIP(hipEventSynchronize(t_nan.ev));
+    *has_nan = *t_nan.host ? 1 : 0;
+    t_nan.armed = false;
     return DDR_OK;
   })
 }

@@ -311,6 +311,7 @@ ddr_status upload_schedule_async(Graph* g, hipStream_t stream);
 constexpr int64_t kStatusBytes = 256;
 constexpr int kStatusTicketFwd = 2;
 constexpr int kStatusTicketBwd = 3;
+constexpr int kStatusNaN = 4;  // DDR_FWD_CHECK_QPRIME: a NaN in the flow-scaled q' the window reads
 // RouteArgs.flags bits beyond the public DDR_FWD_* flags
 constexpr int32_t kFlagForceTimeout = 1 << 16;  // debug: every inter-workgroup wait times out
 constexpr int32_t kFlagNoSteady = 1 << 17;      // debug / A/B: every tick through the general path

@@ -607,34 +607,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     }
   };
 
-  auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR], auto sc) {
-    constexpr bool kSt = decltype(sc)::value;
-    if constexpr (KR == 1) {
-      // a storer wave issues no q' loads: it never waits for its stores (its import owners wait only for
-      // their granules, requested before this tick's stores -- store_pass runs after the import)
-      if (!storer_wave) {
-#if DDR_FWD_TOPWAIT
-        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-#endif
-      }
-    } else {
-#if DDR_FWD_TOPWAIT
-      // the previous tick's q' prefetch and stores land here (see the backward kernel's tick)
-      __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-#endif
-    }
-    phz.mark(0);  // the previous tick's loads and stores
-    // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
-    // instead of being hoisted into registers held across the loop
-    const int tq = opq(tid);
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      ref[k] = opq(ref[k]);
-      off[k] = opq(off[k]);
-      up[k] = opq(up[k]);
-      ex[k] = opq(ex[k]);
-      inv[k] = opq(inv[k]);
-    }
+  // the import of the next chunk of every virtual inflow, at ticks tau = 0 mod kChunkFwd (owners only)
+  auto import_chunk = [&](int tau) {
     if (B.nvirt > 0 && (tau % kChunkFwd) == 0) {
       // import the next chunk of every virtual inflow (x of the upstream block's reach): its owner
       // thread requests the kChunkFwd granules at once
@@ -688,10 +662,38 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (DDR_FWD_IMPORT_BARRIER) lds_barrier();
       if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
-    phz.mark(1);  // import
-    if constexpr (KR == 1) {
-      if (storer_wave && tau > 0) store_pass(tau - 1);
+  };
+  // a virtual inflow's value of tick tau into its slot of buffer `dst` (owners only)
+  auto publish_virt = [&](int tau, double* dst) {
+    if (vown) {
+      const int t = tau - v_off;
+      if (t >= 0 && t < T) dst[B.nloc + vi] = ring[vi * kChunkFwd + (tau % kChunkFwd)];
     }
+  };
+
+  // One tick of the waves that route reaches (every wave outside storer mode)
+  auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR], auto sc) {
+    constexpr bool kSt = decltype(sc)::value;
+#if DDR_FWD_TOPWAIT
+    // the previous tick's q' prefetch and stores land here (see the backward kernel's tick); unconditional,
+    // so the compiler's own wait analysis sees no load outstanding past it (a wait it could not prove made
+    // it wait again, vmcnt(0), at the first use of qcur -- after this tick's prefetch was issued)
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#endif
+    phz.mark(0);  // the previous tick's loads and stores
+    // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
+    // instead of being hoisted into registers held across the loop
+    const int tq = opq(tid);
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      ref[k] = opq(ref[k]);
+      off[k] = opq(off[k]);
+      up[k] = opq(up[k]);
+      ex[k] = opq(ex[k]);
+      inv[k] = opq(inv[k]);
+    }
+    import_chunk(tau);
+    phz.mark(1);  // import
     prefetch(tau + 1, qnext, tq, sc);
     R* xrow = xsave + xs_base + (int64_t)tau * B.nloc;  // this tick's row of the state layout
     double xk[KR];
@@ -717,6 +719,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       ReachStatic<R> st[NP];
       R Qv[NP];
       PhysOut<R> ph[NP];
+      // the upstream slots first: they do not depend on the physics, so their LDS latency hides under it
+      // (the second upstream's slot is the packed word's f1; a confluence's comes from its list below)
+      double x0a[NP], x1a[NP];
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {
+        x0a[h] = sxr[up_0(up[k0 + h])];
+        x1a[h] = sxr[up_n(up[k0 + h]) > 2 ? S - 1 : up_f1(up[k0 + h])];  // (a list offset is not a slot)
+      }
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
         const int r = tq + (k0 + h) * BS;
@@ -748,8 +758,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
         const R qc = rmax(qv, cs.qlb);                                        // mmc.py:421-424
         const R b = ((ph[h].c2 * In[k]) + (ph[h].c3 * Q[k])) + (ph[h].c4 * qc);  // mmc.py:535-538
-        const double x0v = sxr[up_0(up[k])];
-        const double x1v = sxr[up_1(up[k], xl)];
+        const double x0v = x0a[h];
+        double x1v = x1a[h];
+        if (nup > 2) x1v = sxr[xl[up_f1(up[k]) + 1]];  // a confluence: its list [c, u1, ...]
         // Q_j(t) of the upstream reaches (mmc.py:557; the carried state at t = 0 is not clamped)
         const bool raw = !kSt && (t == 0 && carry);
         auto qf = [&](double x) -> R {
@@ -821,10 +832,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     }
     if constexpr (kDbl) {
       // the virtual inflows' values of this tick, beside the reaches' (owners only read their own ring)
-      if (vown) {
-        const int t = tau - v_off;
-        if (t >= 0 && t < T) sxw[B.nloc + vi] = ring[vi * kChunkFwd + (tau % kChunkFwd)];
-      }
+      publish_virt(tau, sxw);
       phz.mark(2);  // prefetch issue + compute + publish
       lds_barrier();
       phz.mark(3);  // the tick's one barrier
@@ -841,16 +849,35 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int r = tq + k * BS;
       if (r < B.nloc && (kSt || (t >= 0 && t < T))) sx[r] = xk[k];
     }
-    if (vown) {
-      const int t = tau - v_off;
-      if (t >= 0 && t < T) sx[B.nloc + vi] = ring[vi * kChunkFwd + (tau % kChunkFwd)];
-    }
+    publish_virt(tau, sx);
     phz.mark(4);  // publish
     lds_barrier();
     phz.mark(5);  // barrier 2
   };
 
   const int TT = (int)T + B.dmax;
+  if constexpr (KR == 1) {
+    if (storer_wave) {
+      // Storer waves (storer mode: the upper half of the workgroup): their own loop -- the import of the
+      // virtual inflows they own, the stores of the x their reach published a tick earlier, the virtuals'
+      // publish and the tick's barriers -- so the routing waves' tick carries no storer branch
+#pragma unroll 1
+      for (int tau = 0; tau < TT; ++tau) {
+        import_chunk(tau);
+        if (tau > 0) store_pass(tau - 1);
+        if constexpr (kDbl) {
+          publish_virt(tau, sx + (tau & 1) * S);
+          lds_barrier();
+        } else {
+          lds_barrier();
+          publish_virt(tau, sx);
+          lds_barrier();
+        }
+      }
+      store_pass(TT - 1);  // the last tick's publish (its barrier has passed)
+      return;
+    }
+  }
   using Gen = std::integral_constant<bool, false>;
   using Steady = std::integral_constant<bool, true>;
   prefetch(0, qa, tid, Gen{});
@@ -892,9 +919,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
 #endif
-  if constexpr (KR == 1) {
-    if (storer_wave) store_pass(TT - 1);  // the last tick's publish (its barrier has passed)
-  }
   if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
   phz.flush(a.prof, a.nblocks, bid);
 }
@@ -1033,6 +1057,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // they have the whole tick to land instead of the part after the first barrier
   R xb2[KR];
   constexpr bool kEarly = DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR;
+  // gauge mode, KR <= 2: each reach's gauge when it has exactly one (else -1: none, or several -- the
+  // reach -> gauge list is walked), so the tick's dL/dout loads are one address computation, not a chain of
+  // three dependent loads each followed by a wait
+  constexpr bool kGReg = KR <= 2;
+  int gsg[kGReg ? KR : 1];
   R qsv[GS ? KR : 1];  // state gradients: q' * flow_scale of this tick's step (prefetched a tick ahead)
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
@@ -1044,6 +1073,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
     const bool nograd = a.g_roff != nullptr && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]];
+    if constexpr (kGReg) {
+      gsg[k] = -1;
+      if (a.g_roff != nullptr && a.g_roff[ref[k] + 1] - a.g_roff[ref[k]] == 1) gsg[k] = (int)a.g_rg[a.g_roff[ref[k]]];
+    }
     od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu) | (nograd ? 0x80000000u : 0u);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
     lam[k] = sxn[k] = R(0);
@@ -1126,7 +1159,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
   // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439)
-  auto load_grad = [&](int ref, int64_t base) {
+  auto load_grad = [&](int ref, int64_t base, int gs) {
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
     const int64_t i1 = base + 1 < T ? base + 1 : T - 1, i2 = base + 2 < T ? base + 2 : T - 1,
                   i3 = base + 3 < T ? base + 3 : T - 1;
@@ -1146,6 +1179,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     };
     if (a.g_roff) {
+      if (gs >= 0) {
+        // the reach's only gauge (kGReg): the row address needs no dependent index loads in the tick
+        add_row(gout + (int64_t)gs * T, !(GS && base == 0 && a.gmask0 && a.gmask0[gs] == 0));
+        return make_grad4(v0, v1, v2, v3);
+      }
       const int64_t q1 = a.g_roff[ref + 1];
       for (int64_t q = a.g_roff[ref]; q < q1; ++q) {
         const int64_t gi = a.g_rg[q];
@@ -1374,7 +1412,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = t - 1;
       if (hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
-        const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3));
+        const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3), kGReg ? opq(gsg[kGReg ? k : 0]) : -1);
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -1440,7 +1478,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
   for (int k = 0; k < KR; ++k)
     if (tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
-      const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3));
+      const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1);
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
   phz.start();
@@ -1514,6 +1552,28 @@ __global__ void finish_grads_kernel(int64_t N, const double* gacc, R* gn, R* gq,
 // One workgroup per (block, tile of gather_steps steps): reads walk the block's reaches in
 // ascending reference order (runs of adjacent q' columns), writes walk positions (sorted by tick
 // offset, so runs of one offset are contiguous in a tick row); the tile is staged in LDS.
+// DDR_FWD_CHECK_QPRIME: the reference asserts that the flow-scaled q' holds no NaN before routing
+// (mmc.py:335, `assert ~torch.any(torch.isnan(self.q_prime))`); the gathers see every value the window
+// reads, so they set status word kStatusNaN instead of a separate pass over q' (28 GB at C5)
+__device__ __forceinline__ void flag_nan(const RouteArgs& a, bool nan) {
+  if (!(a.flags & DDR_FWD_CHECK_QPRIME)) return;
+  if (__builtin_amdgcn_ballot_w64(nan) != 0 && (threadIdx.x & 63) == 0) atomicOr(a.status + kStatusNaN, 1u);
+}
+// ... and the one row no routing step reads: q' of the window's last hour (its row (T - 1) / qp_hours)
+template <typename R>
+__global__ void nan_last_row_kernel(RouteArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool nan = false;
+  if (i < a.N) {
+    const int64_t row = (a.T - 1) / (a.qp_hours > 0 ? a.qp_hours : 1);
+    R v = static_cast<const R*>(a.qprime)[row * a.N + i];
+    if (a.qp_valid && !a.qp_valid[i]) v = R(0.001f);
+    if (a.fs) v = v * static_cast<const R*>(a.fs)[i];
+    nan = v != v;
+  }
+  flag_nan(a, nan);
+}
+
 template <typename R, int G>
 __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
@@ -1539,6 +1599,7 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
     rowoff[j] = (t / a.qp_hours) * N;
   }
   const unsigned char* valid = a.qp_valid;
+  bool nan = false;
   // all G loads of a reach are independent and issued together (memory-level parallelism)
 #pragma unroll 2
   for (int i = threadIdx.x; i < nl; i += 1024) {
@@ -1557,8 +1618,12 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
       for (int j = 0; j < G; ++j) v[j] = v[j] * f;
     }
 #pragma unroll
-    for (int j = 0; j < G; ++j) tile[j * nl + loc] = v[j];
+    for (int j = 0; j < G; ++j) {
+      tile[j * nl + loc] = v[j];
+      nan = nan || v[j] != v[j];
+    }
   }
+  flag_nan(a, nan);
   __syncthreads();
   R* qs = static_cast<R*>(a.qs) + T * B.pos0 + B.pre_dn;
   const int* off = a.s.off + B.pos0;
@@ -1613,6 +1678,7 @@ __global__ void __launch_bounds__(1024) gather_qprime_rows_kernel(RouteArgs a) {
   const int* rs_ref = a.s.rs_ref + B.pos0;
   const int jn = (int)(a.qs_rows - d0 < G ? a.qs_rows - d0 : G);
   const unsigned char* valid = a.qp_valid;
+  bool nan = false;
   for (int i = threadIdx.x; i < nl; i += 1024) {
     const int ref = rs_ref[i], loc = rs_loc[i];
     R v[G];
@@ -1628,8 +1694,12 @@ __global__ void __launch_bounds__(1024) gather_qprime_rows_kernel(RouteArgs a) {
       for (int j = 0; j < G; ++j) v[j] = v[j] * f;
     }
 #pragma unroll
-    for (int j = 0; j < G; ++j) tile[j * nl + loc] = v[j];
+    for (int j = 0; j < G; ++j) {
+      tile[j * nl + loc] = v[j];
+      nan = nan || (j < jn && v[j] != v[j]);
+    }
   }
+  flag_nan(a, nan);
   __syncthreads();
   R* qs = static_cast<R*>(a.qs) + (int64_t)a.qs_rows * B.pos0;
   for (int r = threadIdx.x; r < nl; r += 1024) {
@@ -1879,6 +1949,11 @@ hipError_t launch_split_finish(const Graph* g, const RouteArgs& a, hipStream_t s
 template <typename R>
 hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream) {
   if (g->max_nloc == 0 || a.T == 0) return hipSuccess;
+  if (a.flags & DDR_FWD_CHECK_QPRIME) {
+    hipLaunchKernelGGL(nan_last_row_kernel<R>, dim3((unsigned)((a.N + 255) / 256)), dim3(256), 0, stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
 #ifndef DDR_GATHER_G
 #define DDR_GATHER_G 8
 #endif

@@ -98,6 +98,14 @@ def _check_inputs(qprime, tensors, p=None):
         raise ValueError(f"p_spatial has {p.numel()} elements: expected 1 or {N}")
 
 
+def qprime_has_nan() -> bool:
+    """Whether the calling thread's last ``route(..., check_qprime=True)`` saw a NaN in its q' (waits for
+    that launch's q' gather, not for its routing kernel)."""
+    v = C.c_int32()
+    _lib.check(_lib.load().ddr_qprime_nan_wait(C.byref(v)))
+    return bool(v.value)
+
+
 def check_status(wait: bool = True) -> None:
     """Raise ``DDRError(DDR_ERR_TIMEOUT)`` if an earlier routing launch had a timed-out
     inter-workgroup hand-off (its outputs hold NaN).  Without ``wait`` only launches that have
@@ -371,7 +379,7 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
           q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
           save: bool | None = None, steps: int | None = None, qprime_hours: int = 1,
           qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False,
-          fast_math: bool = False, math: str | None = None):
+          fast_math: bool = False, math: str | None = None, check_qprime: bool = False):
     """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last).
 
     ``math`` (fp32 forward): ``"exact"`` (default) -- the reference's operation order, IEEE division,
@@ -388,7 +396,11 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
     ``qprime_hours`` = 24 with ``steps`` = T routes a daily store (ceil(T / 24), N) indexed in-kernel
     (readers.py:513-519); ``qprime_valid`` (N, bool) marks divides present in the store, the others get
     0.001 (readers.py:523-530).  ``daily`` (gauge mode) returns the fused daily objective series
-    (G, D).  ``accumulate`` makes every step a hot start (geometry_predictor.py:193-212)."""
+    (G, D).  ``accumulate`` makes every step a hot start (geometry_predictor.py:193-212).
+
+    ``check_qprime``: the q' gather also tests the window's flow-scaled q' for NaN (the reference's
+    cold-start assertion, mmc.py:335); :func:`qprime_has_nan` then returns the verdict, waiting for the
+    gather only."""
     dt = qprime.dtype
     dev = qprime.device
 
@@ -407,7 +419,8 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
         raise ValueError(f"math must be 'exact', 'faithful' or 'fast', not {math!r}")
     flags = ((_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
              | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0) | (_lib.DDR_FWD_FAST_MATH if math == "fast" else 0)
-             | (_lib.DDR_FWD_FAITHFUL_MATH if math == "faithful" else 0))
+             | (_lib.DDR_FWD_FAITHFUL_MATH if math == "faithful" else 0)
+             | (_lib.DDR_FWD_CHECK_QPRIME if check_qprime else 0))
     valid = None if qprime_valid is None else qprime_valid.to(device=dev, dtype=torch.uint8).contiguous()
     gid = register_graph(graph)
     gz = gauges

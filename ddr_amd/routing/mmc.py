@@ -21,7 +21,7 @@ from typing import Any
 import torch
 
 from ..graph import RiverGraph, adjacency_to_coo
-from ..ops import GaugeMap, RouteConsts, route
+from ..ops import GaugeMap, RouteConsts, qprime_has_nan, route
 from .utils import PatternMapper, denormalize, get_network_idx, triangular_sparse_solve
 
 log = logging.getLogger(__name__)
@@ -79,6 +79,13 @@ def compute_hotstart_discharge(q_prime_t0: torch.Tensor, mapper: PatternMapper, 
     return torch.clamp(discharge, min=discharge_lb)
 
 
+def _assert_no_nan(q_prime: torch.Tensor) -> None:
+    """mmc.py:335 on the host: one reduction pass (a NaN makes the sum NaN); the elementwise check only
+    decides the rare NaN-sum case (+inf and -inf)."""
+    if bool(torch.isnan(q_prime.sum())):
+        assert ~torch.any(torch.isnan(q_prime)), "q_prime has NaN flows"
+
+
 def _apply_data_override(derived: torch.Tensor, data: torch.Tensor | None) -> torch.Tensor:
     """Observed geometry replaces the power-law one where available (mmc.py:74-99)."""
     if data is None or data.numel() == 0:
@@ -101,8 +108,10 @@ class MuskingumCunge:
     @property
     def _discharge_t(self) -> torch.Tensor | None:
         if self._hot_pending is not None:
-            mapper, qp = self._hot_pending  # (the q' of the setup_inputs that made the cold start)
+            qp = self._hot_pending  # (the q' of the setup_inputs that made the cold start)
             self._hot_pending = None
+            _assert_no_nan(qp)
+            mapper, _, _ = self.create_pattern_mapper()
             self._state = compute_hotstart_discharge(qp[0].to(self.device), mapper, self.discharge_lb, self.device)
         return self._state
 
@@ -126,7 +135,7 @@ class MuskingumCunge:
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None
-        self._hot_pending: tuple | None = None  # (mapper, q') of a cold start whose hot start has not run yet
+        self._hot_pending: torch.Tensor | None = None  # the q' of a cold start whose hot start has not run yet
         self._state: torch.Tensor | None = None
         self._discharge_t = None
         self.network: torch.Tensor | None = None
@@ -216,15 +225,14 @@ class MuskingumCunge:
         if carry_state and (self._state is not None or self._hot_pending is not None):
             return
         assert self.q_prime is not None, "q_prime must be set before initializing discharge state"
-        # mmc.py:335 -- one reduction pass over q' (a NaN makes the sum NaN); the elementwise check
-        # (which materialises a (T, N) mask) only decides the rare NaN-sum case (+inf and -inf)
-        if bool(torch.isnan(self.q_prime.sum())):
-            assert ~torch.any(torch.isnan(self.q_prime)), "q_prime has NaN flows"
-        mapper, _, _ = self.create_pattern_mapper()
-        if getattr(mapper, "graph", None) is not None:
+        if self._graph is not None:
+            # forward's launch runs the hot start as its step 0 and the NaN assertion of mmc.py:335 inside
+            # its q' gather (no separate pass over q'); reading _discharge_t first runs both here
             self._state = None
-            self._hot_pending = (mapper, self.q_prime)  # forward's launch runs it, or the first read of _discharge_t
+            self._hot_pending = self.q_prime
         else:
+            _assert_no_nan(self.q_prime)
+            mapper, _, _ = self.create_pattern_mapper()
             self._discharge_t = compute_hotstart_discharge(self.q_prime[0].to(self.device), mapper,
                                                            self.discharge_lb, self.device)
 
@@ -262,11 +270,14 @@ class MuskingumCunge:
                                "construct it with a cuda device")
         qp = self.q_prime.to(torch.float32)
         # a pending cold start of this q': the launch's own step 0 is the hot start (mmc.py:25-66, 385, 412)
-        own = self._hot_pending is not None and self._hot_pending[1] is self.q_prime
+        own = self._hot_pending is not None and self._hot_pending is self.q_prime
         q0 = None if own else self._discharge_t
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
                                        self.slope, self.x_storage, q0=q0, gauges=self._gauges,
-                                       consts=self._consts(), math=self.math)
+                                       consts=self._consts(), math=self.math, check_qprime=own)
+        # mmc.py:335 (the cold start's assertion), decided by the launch's q' gather: this waits for the
+        # gather only -- the routing kernel queued behind it keeps running while the host goes on
+        assert not (own and qprime_has_nan()), "q_prime has NaN flows"
         self._discharge_t = q_last  # (also clears the pending cold start)
         if qp.shape[0] > 1:
             self.top_width = _apply_data_override(tw, self._data_top_width)

@@ -229,7 +229,12 @@ typedef struct {
  *   arithmetic (like the reference's own Sleef powf; no fp64 on the chain);
  * DDR_FWD_FAST_MATH: hardware v_rcp / v_log / v_exp throughout (~1e-6 relative per coefficient). */
 enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8, DDR_FWD_FAST_MATH = 16,
-       DDR_FWD_FAITHFUL_MATH = 32 };
+       DDR_FWD_FAITHFUL_MATH = 32, DDR_FWD_CHECK_QPRIME = 64 };
+/* DDR_FWD_CHECK_QPRIME: the forward also tests the flow-scaled q' of the window for NaN (the reference's
+ * cold-start assertion, mmc.py:335) inside its q' gather -- no extra pass over q'.  The verdict of the
+ * calling thread's last such launch: ddr_qprime_nan_wait, which waits for the gather only (an event
+ * recorded behind it), not for the routing kernel queued after it. */
+ddr_status ddr_qprime_nan_wait(int32_t* has_nan);
 
 /* Fused forward over T steps (hot start at t = 0 unless DDR_FWD_CARRY, then q0 is Q_0).
  * Returns DDR_ERR_TIMEOUT instead of launching when an earlier launch's hand-off timed out

@@ -272,7 +272,25 @@ def test_nan_streamflow_asserts_like_the_reference(cuda):
     model = dmc(cfg_of(PARAMS_DEFAULT), device=cuda)
     with pytest.raises(AssertionError, match="NaN flows"):
         model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params)
+    # the check runs inside the forward's q' gather: every row, the last hour's (no step reads it) too,
+    # and a NaN that reading the state first surfaces at that read (the hot start runs there)
+    for row in (0, q.shape[0] - 1):
+        q = torch.from_numpy(case.qprime).clone()
+        q[row, 3] = float("nan")
+        with pytest.raises(AssertionError, match="NaN flows"):
+            model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params)
+        mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
+        mc.setup_inputs(golden_dataclass(case), q, sp_params)
+        with pytest.raises(AssertionError, match="NaN flows"):
+            _ = mc._discharge_t
+    # a carried state skips the check, as in the reference (mmc.py:332-335)
+    q = torch.from_numpy(case.qprime).clone()
+    out = model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params)["runoff"]
+    q[2, 5] = float("nan")
+    model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params, carry_state=True)
+    assert torch.isfinite(out).all()
     q = torch.from_numpy(case.qprime).clone()
     q[5, 3], q[6, 4] = float("inf"), float("-inf")
     mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
     mc.setup_inputs(golden_dataclass(case), q, sp_params)  # no assertion
+    mc.forward()

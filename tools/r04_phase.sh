@@ -18,6 +18,7 @@ timeout -k 10 900 python3 -u -m pytest $R/tests/test_gpu_steady.py $R/tests/test
   --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
 env $S8 timeout -k 10 240 python3 -u $R/bench.py $B --steps 3 --warmup 1 > $O/c3s8_new.json 2> $O/c3s8_new.err || exit 1
+env $S8 DDR_PACK_QUANT=256 timeout -k 10 240 python3 -u $R/bench.py $B --steps 3 --warmup 1 > $O/c3s8_new_q256.json 2> $O/c3s8_new_q256.err || exit 1
 timeout -k 10 300 python3 -u $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps 0 > $O/c5_new.json 2> $O/c5_new.err || exit 1
 env $L03 timeout -k 10 300 python3 -u $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps 0 > $O/c5_r03.json 2> $O/c5_r03.err || exit 1
 timeout -k 10 400 python3 -u $R/tools/dropin_breakdown.py > $O/dropin.json 2> $O/dropin.err || exit 1
