@@ -569,6 +569,9 @@ struct DevBuild {
 
   explicit DevBuild(hipStream_t st) : s(st), scr(st) {}
   ~DevBuild() {
+    // a build that failed after the slab or the staging block was attached: both go back to their pools
+    // stream-ordered (after whatever the build queued on s), not leaked as handed out
+    if (g) destroy_graph(g.release(), s);
     if (tab_ev) (void)hipEventDestroy(tab_ev);
     pinned_put(pin, s);  // its copies were waited for (read_table), or are queued on s
     pinned_put(ptab, s);

@@ -37,10 +37,39 @@ __device__ __forceinline__ float shfl_xor_f(float v, int m) {
   return __shfl_xor(v, m, 64);
 }
 
-// Ascending bitonic sort of the wave's 64 * KD values, element e = i * 64 + lane in v[i].
+// v of lane ^ J, J a power of two < 64, without the LDS crossbar where a DPP pattern exists (each
+// ds_bpermute is an LDS round trip the bitonic stages then wait for): J = 1, 2 quad permutes; 4 a half-row
+// mirror then a quad reverse ((l ^ 7) ^ 3 = l ^ 4); 8 a row rotate by 8; 16 a swizzle swap; 32 the
+// gfx950 permlane32 swap
+template <int J>
+__device__ __forceinline__ float xor_lane(float v) {
+  const int iv = __float_as_int(v);
+  if constexpr (J == 1) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(iv, 0xB1, 0xF, 0xF, true));  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(iv, 0x4E, 0xF, 0xF, true));  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const int m = __builtin_amdgcn_mov_dpp(iv, 0x141, 0xF, 0xF, true);        // row_half_mirror
+    return __int_as_float(__builtin_amdgcn_mov_dpp(m, 0x1B, 0xF, 0xF, true));  // quad_perm [3,2,1,0]
+  } else if constexpr (J == 8) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(iv, 0x128, 0xF, 0xF, true));  // row_ror:8
+  } else if constexpr (J == 16) {
+    return __int_as_float(__builtin_amdgcn_ds_swizzle(iv, 0x401F));  // swizzle(SWAP, 16)
+  } else {
+    static_assert(J == 32, "lane xor distance");
+    const auto pr = __builtin_amdgcn_permlane32_swap(iv, iv, false, false);
+    return __int_as_float((threadIdx.x & 32) ? pr[0] : pr[1]);
+  }
+}
+
+// Ascending bitonic sort of the wave's 64 * KD values, element e = i * 64 + lane in v[i].  Each
+// compare-exchange is one v_med3_f32 per element: med3(a, b, -inf) = min, med3(a, b, +inf) = max (no NaN
+// reaches the sort; a min / max pair plus a select, with the IEEE-mode canonicalisations fminf / fmaxf
+// bring, cost 4-5 instructions), the partner in another lane fetched by xor_lane.
 template <int KD>
 __device__ __forceinline__ void wave_sort(float (&v)[KD], int lane) {
   constexpr int M = 64 * KD;
+  const float ninf = -__builtin_inff(), pinf = __builtin_inff();
 #pragma unroll
   for (int k = 2; k <= M; k <<= 1) {
 #pragma unroll
@@ -50,20 +79,32 @@ __device__ __forceinline__ void wave_sort(float (&v)[KD], int lane) {
 #pragma unroll
         for (int i = 0; i < KD; ++i) {
           if (i & jj) continue;
-          const int e = i * 64 + lane;
-          const bool asc = (e & k) == 0;
+          const bool asc = ((i * 64) & k) == 0;  // (k >= 128 here: the lane does not enter)
           const float a = v[i], b = v[i | jj];
-          v[i] = asc ? fminf(a, b) : fmaxf(a, b);
-          v[i | jj] = asc ? fmaxf(a, b) : fminf(a, b);
+          v[i] = __builtin_amdgcn_fmed3f(a, b, asc ? ninf : pinf);
+          v[i | jj] = __builtin_amdgcn_fmed3f(a, b, asc ? pinf : ninf);
         }
       } else {
         const bool lower = (lane & j) == 0;
+        // every partner fetched before the first exchange: a DPP read of a register the previous VALU
+        // instruction wrote needs wait states (s_nop) the stage's other elements fill instead
+        float o[KD];
+#pragma unroll
+        for (int i = 0; i < KD; ++i) {
+          switch (j) {  // (j is a compile-time constant of the unrolled loop)
+            case 1: o[i] = xor_lane<1>(v[i]); break;
+            case 2: o[i] = xor_lane<2>(v[i]); break;
+            case 4: o[i] = xor_lane<4>(v[i]); break;
+            case 8: o[i] = xor_lane<8>(v[i]); break;
+            case 16: o[i] = xor_lane<16>(v[i]); break;
+            default: o[i] = xor_lane<32>(v[i]); break;
+          }
+        }
 #pragma unroll
         for (int i = 0; i < KD; ++i) {
           const int e = i * 64 + lane;
           const bool asc = (e & k) == 0;
-          const float o = shfl_xor_f(v[i], j);
-          v[i] = (lower == asc) ? fminf(v[i], o) : fmaxf(v[i], o);
+          v[i] = __builtin_amdgcn_fmed3f(v[i], o[i], (lower == asc) ? ninf : pinf);
         }
       }
     }
@@ -121,12 +162,31 @@ __device__ __forceinline__ float geom_var(const DayGeom& g, float Q, int var) {
 // the same min / max / median as a sort of every variable, in every case.  The mean is the fp64 sum of
 // the valid values (fp32 values, so the order does not change it where the range stays within 2^29).
 template <int KD>
+__device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t reach, int lane);
+
+// Persistent workgroups (the math tables are loaded once per workgroup, not once per 4 reaches) over groups
+// of 4 consecutive reaches; the groups are dealt out XCD-major -- workgroup w runs on XCD w % 8 and walks a
+// contiguous range of groups -- so that the reaches sharing a line of the (day, reach) discharge layout are
+// read through one L2, not fetched once per XCD.
+template <int KD>
 __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
   load_math_tables();
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int64_t reach = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (reach >= a.N) return;  // whole waves leave together
+  const int64_t groups = (a.N + 3) / 4;
+  const int64_t nwg = gridDim.x;                 // a multiple of 8
+  const int64_t per_xcd = nwg / 8;
+  const int64_t xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const int64_t span = (groups + 7) / 8;         // groups per XCD, contiguous
+  const int64_t g0 = xcd * span, g1 = g0 + span < groups ? g0 + span : groups;
+  for (int64_t grp = g0 + slot; grp < g1; grp += per_xcd) {
+    const int64_t reach = grp * 4 + (threadIdx.x >> 6);
+    if (reach < a.N) geometry_stats_reach<KD>(a, reach, lane);
+  }
+}
+
+template <int KD>
+__device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t reach, int lane) {
   Consts<float> cs{};
   cs.dt = 3600.0f;
   cs.qlb = 0.0f;
@@ -158,6 +218,11 @@ __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
 #pragma unroll
   for (int i = 0; i < KD; ++i) {
     const bool ok = i * 64 + lane < cq;
+    if (i * 64 >= cq) {  // (wave-uniform) no valid day in this slot: no geometry to evaluate
+#pragma unroll
+      for (int var = 0; var < kGeoVars; ++var) vals[var][i] = __builtin_nanf("");
+      continue;
+    }
     const float Q = ok ? qv[i] : 1.0f;  // (padding: any positive value, the result is discarded)
     const DayGeom g = day_geometry(st, Q, cs);
 #pragma unroll
@@ -171,7 +236,12 @@ __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
     bool inc = true, dec = true;
 #pragma unroll
     for (int i = 0; i < KD; ++i) {
-      const float x = vals[var][i];
+      // (var is not an unrolled index: a select chain keeps vals in registers, where vals[var][i] would
+      // send the array to scratch)
+      const float x = var == 0 ? vals[0][i]
+                               : (var == 1 ? vals[1][i]
+                                           : (var == 2 ? vals[2][i]
+                                                       : (var == 3 ? vals[3][i] : (var == 4 ? vals[4][i] : vals[5][i]))));
       const bool valid = x == x;
       cnt += valid;
       sum += valid ? (double)x : 0.0;
@@ -352,7 +422,11 @@ hipError_t launch_geometry_stats(const float* qd, int64_t rs, int64_t ds, int64_
     hipLaunchKernelGGL(geometry_stats_long_kernel, dim3((unsigned)N), dim3(1024), smem, stream, a, P);
     return hipGetLastError();
   }
-  const dim3 grid((unsigned)((N + 3) / 4)), block(256);
+  // persistent: 8 workgroups of 4 waves per CU at most (256 CUs), a multiple of 8 (the XCD deal)
+  const int64_t groups = (N + 3) / 4;
+  int64_t nwg = std::min<int64_t>(groups, 256 * 8);
+  nwg = (nwg + 7) / 8 * 8;
+  const dim3 grid((unsigned)nwg), block(256);
   if (D <= 64) hipLaunchKernelGGL(geometry_stats_kernel<1>, grid, block, kMathTabBytes, stream, a);
   else if (D <= 128) hipLaunchKernelGGL(geometry_stats_kernel<2>, grid, block, kMathTabBytes, stream, a);
   else if (D <= 256) hipLaunchKernelGGL(geometry_stats_kernel<4>, grid, block, kMathTabBytes, stream, a);

@@ -176,9 +176,11 @@ ddr_status plan_init(int64_t n, int64_t bmax, const ddr_build_opts* opts, PackPl
   P.steps = (opts && opts->steps_hint > 0) ? (double)opts->steps_hint : 8760.0;
   // exponent of the chain-pacing weight (T + L) / T (experiments: DDR_PACK_FAC_POW)
   P.fac_pow = getenv("DDR_PACK_FAC_POW") ? atof(getenv("DDR_PACK_FAC_POW")) : 1.0;
-  // block capacity rounded down to a multiple of this many reaches (a tick costs per 256-reach
-  // slice-per-SIMD unit; experiments: DDR_PACK_QUANT)
-  P.pack_quant = getenv("DDR_PACK_QUANT") ? atol(getenv("DDR_PACK_QUANT")) : 1;
+  // block capacity rounded down to a multiple of this many reaches: a tick costs per 256-reach
+  // slice-per-SIMD unit, so at light loads (one reach per thread) a block of 513..523 reaches ticks at the
+  // rate of 768 and loses the storer waves (<= 512) -- C3 8-way shard forward 3.15 -> 2.88 ms; at full
+  // load (C3, C5 on one GPU) no gain, off (profiles/r04/ab_r04.txt; DDR_PACK_QUANT overrides)
+  P.pack_quant = getenv("DDR_PACK_QUANT") ? atol(getenv("DDR_PACK_QUANT")) : (P.cap <= kBlockThreads ? 256 : 1);
   // Split threshold (pieces up to scap_pct % of the capacity): with a dominant basin (C4/C5: 0.35 N)
   // its chain of pieces is the critical path, and pieces at 80 % leave the packer room to give chain
   // blocks fewer reaches; without one (C3: 256 basins of at most 2 % of N) pieces at the full
