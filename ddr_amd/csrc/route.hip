@@ -1574,8 +1574,8 @@ __global__ void nan_last_row_kernel(RouteArgs a) {
   flag_nan(a, nan);
 }
 
-template <typename R, int G>
-__global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
+template <typename R, int G, int BS>
+__global__ void __launch_bounds__(BS) gather_qprime_kernel(RouteArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
   R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
   if (a.owned && !a.owned[blockIdx.x]) return;  // split basin: another rank's block
@@ -1602,7 +1602,7 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   bool nan = false;
   // all G loads of a reach are independent and issued together (memory-level parallelism)
 #pragma unroll 2
-  for (int i = threadIdx.x; i < nl; i += 1024) {
+  for (int i = threadIdx.x; i < nl; i += BS) {
     const int ref = rs_ref[i], loc = rs_loc[i];
     R v[G];
 #pragma unroll
@@ -1628,7 +1628,7 @@ __global__ void __launch_bounds__(1024) gather_qprime_kernel(RouteArgs a) {
   R* qs = static_cast<R*>(a.qs) + T * B.pos0 + B.pre_dn;
   const int* off = a.s.off + B.pos0;
   const int jn = (int)(T - t0 < G ? T - t0 : G);
-  for (int r = threadIdx.x; r < nl; r += 1024) {
+  for (int r = threadIdx.x; r < nl; r += BS) {
     const int64_t o = off[r];
 #pragma unroll
     for (int j = 0; j < G; ++j)
@@ -1967,12 +1967,27 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
                        stream, a);
     return hipGetLastError();
   }
-  auto kern = gather_qprime_kernel<R, G>;
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  if (e != hipSuccess) return e;
-  const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + G - 1) / G));
-  hipLaunchKernelGGL(kern, grid, dim3(1024), smem, stream, a);
-  return hipGetLastError();
+  // light loads (small blocks): more steps per workgroup and 256-thread workgroups -- a workgroup of
+  // 8 steps over a few hundred reaches moved ~20 KB, and the launch was paced by workgroup turnover
+  // (3.2 ms for a 69k-reach C5 shard, 1.5 TB/s)
+  auto launch = [&](auto kern, int gsteps, int bs) -> hipError_t {
+    const size_t sm = (size_t)gsteps * g->max_nloc * sizeof(R);
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    if (e != hipSuccess) return e;
+    const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + gsteps - 1) / gsteps));
+    hipLaunchKernelGGL(kern, grid, dim3(bs), sm, stream, a);
+    return hipGetLastError();
+  };
+  static const int gsel = [] {
+    const char* v = getenv("DDR_GATHER_SEL");
+    return v ? atoi(v) : 1;
+  }();
+  if constexpr (sizeof(R) == 4) {
+    if (gsel && g->max_nloc <= 256) return launch(gather_qprime_kernel<R, 32, 256>, 32, 256);
+    if (gsel && g->max_nloc <= 512) return launch(gather_qprime_kernel<R, 32, 512>, 32, 512);
+    if (gsel && g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
+  }
+  return launch(gather_qprime_kernel<R, G, 1024>, G, 1024);
 }
 
 template <typename R>
