@@ -62,6 +62,30 @@ __device__ __forceinline__ float xor_lane(float v) {
   }
 }
 
+// v of lane (lane + 1) & 63 (DPP wave_rol:1)
+__device__ __forceinline__ float next_lane(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x134, 0xF, 0xF, true));
+}
+// the wave's sum of x (fp64; every lane gets it), by lane-xor exchanges of the two halves
+template <int J>
+__device__ __forceinline__ double xor_lane_d(double x) {
+  const unsigned long long u = __double_as_longlong(x);
+  const float lo = xor_lane<J>(__uint_as_float((unsigned)u));
+  const float hi = xor_lane<J>(__uint_as_float((unsigned)(u >> 32)));
+  return __longlong_as_double((long long)(((unsigned long long)__float_as_uint(hi) << 32) | __float_as_uint(lo)));
+}
+__device__ __forceinline__ double wave_sum(double x) {
+  x += xor_lane_d<1>(x);
+  x += xor_lane_d<2>(x);
+  x += xor_lane_d<4>(x);
+  x += xor_lane_d<8>(x);
+  x += xor_lane_d<16>(x);
+  x += xor_lane_d<32>(x);
+  return x;
+}
+// number of lanes with p set
+__device__ __forceinline__ int wave_count(bool p) { return __builtin_popcountll(__builtin_amdgcn_ballot_w64(p)); }
+
 // Ascending bitonic sort of the wave's 64 * KD values, element e = i * 64 + lane in v[i].  Each
 // compare-exchange is one v_med3_f32 per element: med3(a, b, -inf) = min, med3(a, b, +inf) = max (no NaN
 // reaches the sort; a min / max pair plus a select, with the IEEE-mode canonicalisations fminf / fmaxf
@@ -111,6 +135,55 @@ __device__ __forceinline__ void wave_sort(float (&v)[KD], int lane) {
   }
 }
 
+// Ascending sort of 64 * KD values of which only the first KE slots can be finite (slots KE.. are +inf
+// padding): KD = 8, KE = 6 (a 365-day year) sorts slots 0-3 and 4-5 separately, lays the second run out
+// descending behind 128 padding values (a bitonic sequence) and merges -- 272 slot-stages instead of the
+// full network's 360.  Other shapes take the full network.
+template <int KD, int KE>
+__device__ __forceinline__ void wave_sort_valid(float (&v)[KD], int lane) {
+  if constexpr (KD == 8 && KE == 6) {
+    const float pinf = __builtin_inff(), ninf = -__builtin_inff();
+    float lo[4] = {v[0], v[1], v[2], v[3]};
+    float hi[2] = {-v[4], -v[5]};  // ascending -w is descending w (+inf padding first)
+    wave_sort<4>(lo, lane);
+    wave_sort<2>(hi, lane);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = pinf; v[5] = pinf; v[6] = -hi[0]; v[7] = -hi[1];
+    // bitonic merge (ascending) of the 512-element bitonic sequence
+#pragma unroll
+    for (int j = 256; j >= 64; j >>= 1) {
+      const int jj = j >> 6;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i & jj) continue;
+        const float a = v[i], b = v[i | jj];
+        v[i] = __builtin_amdgcn_fmed3f(a, b, ninf);
+        v[i | jj] = __builtin_amdgcn_fmed3f(a, b, pinf);
+      }
+    }
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+      const bool lower = (lane & j) == 0;
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        switch (j) {
+          case 1: o[i] = xor_lane<1>(v[i]); break;
+          case 2: o[i] = xor_lane<2>(v[i]); break;
+          case 4: o[i] = xor_lane<4>(v[i]); break;
+          case 8: o[i] = xor_lane<8>(v[i]); break;
+          case 16: o[i] = xor_lane<16>(v[i]); break;
+          default: o[i] = xor_lane<32>(v[i]); break;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = __builtin_amdgcn_fmed3f(v[i], o[i], lower ? ninf : pinf);
+    }
+  } else {
+    wave_sort<KD>(v, lane);
+  }
+}
+
 // Element `idx` (wave-uniform) of the sorted values.
 template <int KD>
 __device__ __forceinline__ float wave_elem(const float (&v)[KD], int idx) {
@@ -119,7 +192,7 @@ __device__ __forceinline__ float wave_elem(const float (&v)[KD], int idx) {
 #pragma unroll
   for (int k = 1; k < KD; ++k)
     if (i == k) r = v[k];
-  return __shfl(r, l, 64);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(r), l));  // (idx is wave-uniform)
 }
 
 // The trapezoid geometry of one day (trapezoidal.py:62-97): coefficients<float, false>'s operations, in its
@@ -142,7 +215,7 @@ __device__ __forceinline__ DayGeom day_geometry(const ReachStatic<float>& s, flo
   const float bwr = g.tw - (2.0f * g.ss) * g.depth;
   g.bw = rmax(bwr, c.bwlb);
   const float area = ((g.tw + g.bw) * g.depth) * 0.5f;
-  const float sq = sqf<false>(1.0f + g.ss * g.ss);
+  const float sq = sqrt_rn_normal(1.0f + g.ss * g.ss);
   const float wp = g.bw + (2.0f * g.depth) * sq;
   g.Rh = dvf<false>(area, wp);
   return g;
@@ -161,14 +234,16 @@ __device__ __forceinline__ float geom_var(const DayGeom& g, float Q, int var) {
 // every adjacent pair and sorts only a variable that is not (or has a NaN where Q is valid).  Exact:
 // the same min / max / median as a sort of every variable, in every case.  The mean is the fp64 sum of
 // the valid values (fp32 values, so the order does not change it where the range stays within 2^29).
-template <int KD>
+template <int KD, int KE>
 __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t reach, int lane);
 
 // Persistent workgroups (the math tables are loaded once per workgroup, not once per 4 reaches) over groups
 // of 4 consecutive reaches; the groups are dealt out XCD-major -- workgroup w runs on XCD w % 8 and walks a
 // contiguous range of groups -- so that the reaches sharing a line of the (day, reach) discharge layout are
 // read through one L2, not fetched once per XCD.
-template <int KD>
+// KE = ceil(D / 64) <= KD: the slots that can hold a day (the sort pads to KD with +inf; everything after
+// it works on the KE slots).
+template <int KD, int KE>
 __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
   load_math_tables();
   __syncthreads();
@@ -181,11 +256,11 @@ __global__ void __launch_bounds__(256) geometry_stats_kernel(GeoArgs a) {
   const int64_t g0 = xcd * span, g1 = g0 + span < groups ? g0 + span : groups;
   for (int64_t grp = g0 + slot; grp < g1; grp += per_xcd) {
     const int64_t reach = grp * 4 + (threadIdx.x >> 6);
-    if (reach < a.N) geometry_stats_reach<KD>(a, reach, lane);
+    if (reach < a.N) geometry_stats_reach<KD, KE>(a, reach, lane);
   }
 }
 
-template <int KD>
+template <int KD, int KE>
 __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t reach, int lane) {
   Consts<float> cs{};
   cs.dt = 3600.0f;
@@ -206,17 +281,15 @@ __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t r
 #pragma unroll
   for (int i = 0; i < KD; ++i) {
     const int64_t d = (int64_t)i * 64 + lane;
-    const float Q = d < a.D ? a.qd[reach * a.rs + d * a.ds] : __builtin_nanf("");
+    const float Q = (i < KE && d < a.D) ? a.qd[reach * a.rs + d * a.ds] : __builtin_nanf("");
     const bool valid = Q == Q;  // torch propagates a NaN discharge through every variable
-    cq += valid;
+    cq += wave_count(valid);
     qv[i] = valid ? Q : __builtin_inff();  // NaN (and the padding) sorts last, past the valid count
   }
+  wave_sort_valid<KD, KE>(qv, lane);
+  float vals[kGeoVars][KE];
 #pragma unroll
-  for (int m = 1; m < 64; m <<= 1) cq += __shfl_xor(cq, m, 64);
-  wave_sort<KD>(qv, lane);
-  float vals[kGeoVars][KD];
-#pragma unroll
-  for (int i = 0; i < KD; ++i) {
+  for (int i = 0; i < KE; ++i) {
     const bool ok = i * 64 + lane < cq;
     if (i * 64 >= cq) {  // (wave-uniform) no valid day in this slot: no geometry to evaluate
 #pragma unroll
@@ -235,7 +308,9 @@ __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t r
     double sum = 0.0;
     bool inc = true, dec = true;
 #pragma unroll
-    for (int i = 0; i < KD; ++i) {
+    for (int i = KE; i < KD; ++i) v[i] = __builtin_inff();  // (sort padding only)
+#pragma unroll
+    for (int i = 0; i < KE; ++i) {
       // (var is not an unrolled index: a select chain keeps vals in registers, where vals[var][i] would
       // send the array to scratch)
       const float x = var == 0 ? vals[0][i]
@@ -243,25 +318,22 @@ __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t r
                                            : (var == 2 ? vals[2][i]
                                                        : (var == 3 ? vals[3][i] : (var == 4 ? vals[4][i] : vals[5][i]))));
       const bool valid = x == x;
-      cnt += valid;
+      cnt += wave_count(valid);
       sum += valid ? (double)x : 0.0;
       v[i] = x;
     }
     // adjacent pairs (e, e + 1), e + 1 < cq: element e + 1 is lane + 1's v[i] (lane 0's v[i + 1] for lane 63)
+    float nx[KE];  // element e + 1 of lane l's element e = i * 64 + l: lane l + 1's v[i], or lane 0's v[i + 1]
 #pragma unroll
-    for (int i = 0; i < KD; ++i) {
-      const float s0 = __shfl(v[i], (lane + 1) & 63, 64);
-      const float s1 = i + 1 < KD ? __shfl(v[i + 1], 0, 64) : 0.0f;
-      const float nb = lane < 63 ? s0 : s1;
+    for (int i = 0; i < KE; ++i) nx[i] = next_lane(v[i]);
+#pragma unroll
+    for (int i = 0; i < KE; ++i) {
+      const float nb = lane < 63 ? nx[i] : (i + 1 < KE ? nx[i + 1] : 0.0f);
       const bool pair = i * 64 + lane + 1 < cq;
       inc = inc && (!pair || v[i] <= nb);
       dec = dec && (!pair || v[i] >= nb);
     }
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-      cnt += __shfl_xor(cnt, m, 64);
-      sum += __shfl_xor(sum, m, 64);
-    }
+    sum = wave_sum(sum);
     const bool all_inc = __builtin_amdgcn_ballot_w64(!inc) == 0;
     const bool all_dec = __builtin_amdgcn_ballot_w64(!dec) == 0;
     float mn, mx, med, mean;
@@ -279,8 +351,8 @@ __device__ __forceinline__ void geometry_stats_reach(const GeoArgs& a, int64_t r
       } else {
         // not monotone along Q (or NaN where Q is valid): sort this variable
 #pragma unroll
-        for (int i = 0; i < KD; ++i) v[i] = v[i] == v[i] ? v[i] : __builtin_inff();
-        wave_sort<KD>(v, lane);
+        for (int i = 0; i < KE; ++i) v[i] = v[i] == v[i] ? v[i] : __builtin_inff();
+        wave_sort_valid<KD, KE>(v, lane);
         i_mn = 0;
         i_mx = cnt - 1;
         i_lo = (cnt - 1) / 2;
@@ -352,10 +424,8 @@ __global__ void __launch_bounds__(1024) geometry_stats_long_kernel(GeoArgs a, in
       v[i] = valid ? x : __builtin_inff();
     }
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-      cnt += __shfl_xor(cnt, m, 64);
-      sum += __shfl_xor(sum, m, 64);
-    }
+    for (int m = 1; m < 64; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
+    sum = wave_sum(sum);
     if (lane == 0) {
       rs[wave] = sum;
       rc[wave] = cnt;
@@ -422,16 +492,29 @@ hipError_t launch_geometry_stats(const float* qd, int64_t rs, int64_t ds, int64_
     hipLaunchKernelGGL(geometry_stats_long_kernel, dim3((unsigned)N), dim3(1024), smem, stream, a, P);
     return hipGetLastError();
   }
-  // persistent: 8 workgroups of 4 waves per CU at most (256 CUs), a multiple of 8 (the XCD deal)
+  // persistent: the resident workgroup count (occupancy x CUs; a grid beyond it would run its extra
+  // workgroups' whole shares after the first ones), rounded down to a multiple of 8 (the XCD deal)
   const int64_t groups = (N + 3) / 4;
-  int64_t nwg = std::min<int64_t>(groups, 256 * 8);
-  nwg = (nwg + 7) / 8 * 8;
-  const dim3 grid((unsigned)nwg), block(256);
-  if (D <= 64) hipLaunchKernelGGL(geometry_stats_kernel<1>, grid, block, kMathTabBytes, stream, a);
-  else if (D <= 128) hipLaunchKernelGGL(geometry_stats_kernel<2>, grid, block, kMathTabBytes, stream, a);
-  else if (D <= 256) hipLaunchKernelGGL(geometry_stats_kernel<4>, grid, block, kMathTabBytes, stream, a);
-  else hipLaunchKernelGGL(geometry_stats_kernel<8>, grid, block, kMathTabBytes, stream, a);
-  return hipGetLastError();
+  const dim3 block(256);
+  auto launch = [&](auto kern) -> hipError_t {
+    int per_cu = 0, dev = 0, cus = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, kMathTabBytes);
+    if (e == hipSuccess) e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    int64_t nwg = std::min<int64_t>(groups, (int64_t)std::max(per_cu, 1) * std::max(cus, 8));
+    nwg = std::max<int64_t>(nwg / 8 * 8, 8);
+    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), block, kMathTabBytes, stream, a);
+    return hipGetLastError();
+  };
+  if (D <= 64) return launch(geometry_stats_kernel<1, 1>);
+  if (D <= 128) return launch(geometry_stats_kernel<2, 2>);
+  if (D <= 192) return launch(geometry_stats_kernel<4, 3>);
+  if (D <= 256) return launch(geometry_stats_kernel<4, 4>);
+  if (D <= 320) return launch(geometry_stats_kernel<8, 5>);
+  if (D <= 384) return launch(geometry_stats_kernel<8, 6>);
+  if (D <= 448) return launch(geometry_stats_kernel<8, 7>);
+  return launch(geometry_stats_kernel<8, 8>);
 }
 
 }  // namespace ddr

@@ -426,9 +426,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #ifndef DDR_FWD_NP_FAST
 #define DDR_FWD_NP_FAST 1
 #endif
+  // faithful: slice pairs in packed halves (coefficients_faithful2)
+#ifndef DDR_FWD_NP_FAITH
+#define DDR_FWD_NP_FAITH 1
+#endif
   constexpr bool kFast = MATH == 1 && std::is_same<R, float>::value;
   constexpr bool kFaith = MATH == 2 && std::is_same<R, float>::value;
-  constexpr int NPW = kFast ? DDR_FWD_NP_FAST : DDR_FWD_NP;
+  constexpr int NPW = kFast ? DDR_FWD_NP_FAST : (kFaith ? DDR_FWD_NP_FAITH : DDR_FWD_NP);
   constexpr int NP = KR < NPW ? KR : NPW;  // slices whose physics runs in lockstep
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bid = take_ticket(a.status, kStatusTicketFwd, a.nblocks, false, reinterpret_cast<int*>(smem));
@@ -739,8 +743,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
           for (int h = 0; h < NP; ++h) ph[h] = coefficients_fast(st[h], Qv[h], cs);
         } else if constexpr (kFaith) {
+          if constexpr (NP == 2) {
+            // the pair's physics in packed halves (the same bits as two scalar evaluations)
+            coefficients_faithful2(st[0], st[1], Qv[0], Qv[1], cs, ph[0], ph[1]);
+          } else {
 #pragma unroll
-          for (int h = 0; h < NP; ++h) ph[h] = coefficients_faithful(st[h], Qv[h], cs);
+            for (int h = 0; h < NP; ++h) ph[h] = coefficients_faithful(st[h], Qv[h], cs);
+          }
         } else {
           coefficients_np<R, NP>(st, Qv, cs, ph);
         }
@@ -976,6 +985,12 @@ __global__ void __launch_bounds__(256) route_last_kernel(RouteArgs a) {
   }
 }
 
+// one reach-step's adjoint outputs: coefficients, dL/dQ_{t-1} and the parameter gradient terms
+template <typename R>
+struct AdjOutR {
+  R c1, c2, c3, c4, gQ, gn, gq, gp;
+};
+
 template <typename R>
 struct Grad4 {
   R a, b, c, d;
@@ -1066,6 +1081,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
   ReachStatic<R> sreg[kStatReg ? KR : 1];
+  // slice pairs whose adjoint steps run in packed halves (fp32 adjoint, KR >= 2)
+#ifndef DDR_BWD_PAIR
+#define DDR_BWD_PAIR 0
+#endif
+  constexpr int NPB = (DDR_BWD_PAIR && KR >= 2 && std::is_same<R, float>::value && !DDR_BWD_EXACT) ? 2 : 1;
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -1315,17 +1335,25 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
     }
     // ---- compute ------------------------------------------------------------------------------
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      if (wbase + k * BS >= B.nloc) continue;
-      const int r = tq + k * BS;
-      const bool hk = r < B.nloc;
-      const int rs = hk ? r : 0;
-      const int t = tau - off_of(k);
-      const bool active = hk && (kSt || (t >= 1 && t < T));
+    // per slice: the step's inputs (pre), its adjoint, its outputs (post) and the next loads (tail);
+    // NPB slices at a time share one packed adjoint (adjoint_step_fast2) when NPB = 2
+    struct Pre {
+      int r, rs, t;
+      bool hk, active, c0;
+      R Sx, I, gk, xtk, lm, gb, Qp;
+      double gb64;
+      ReachStatic<R> st;
+    };
+    auto pre = [&](int k, Pre& P) {
+      P.r = tq + k * BS;
+      P.hk = P.r < B.nloc;
+      P.rs = P.hk ? P.r : 0;
+      P.t = tau - off_of(k);
+      P.active = P.hk && (kSt || (P.t >= 1 && P.t < T));
       // upstream x_j(t - 1): I(t) = sum_j Q_j(t - 1) (mmc.py:535, ascending columns; the carried
       // state at t - 1 = 0 is not clamped) and Sx(t - 1) for the next tick
-      const bool c0 = !kSt && (t == 1 && carry);
+      P.c0 = !kSt && (P.t == 1 && carry);
+      const bool c0 = P.c0;
       const int nup = up_n(up[k]);
       const R x0 = sxr[up_0(up[k])];
       const R x1 = sxr[up_1(up[k], xl)];
@@ -1343,37 +1371,41 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           I = I + (c0 ? xj : rmax(xj, cs.qlb));
         }
       }
-      const R Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
+      P.I = I;
+      P.Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
       sxn[k] = sxv;
-      const int e4 = t & 3;
-      const R gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
-      const R xtk = xc[k];
-      const ReachStatic<R> st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(rs);
-      const R lm = lam[k] + gk;                          // dL/dQ_t (+ dL/dout[:, t])
-      const R gx = (xtk >= cs.qlb) ? lm : R(0);          // clamp backward (inclusive)
-      const double gb64 = (double)gx + (double)A[k];     // (I - C1 N)^T gb = gx (utils.py:188-242)
-      const R gb = R(gb64);
-      const R Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);     // Q_{t-1}
-      // the step's adjoint only where some lane of the wave runs a step this tick (DDR_SKIP_IDLE_BWD)
-      const bool wave_act = !DDR_SKIP_IDLE_BWD || __builtin_amdgcn_ballot_w64(active || (GS && hk && t == 0)) != 0;
-      if (wave_act) {
-      R c1, c2, c3, c4, gQ, gn, gq, gp;
+      const int e4 = P.t & 3;
+      P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+      P.xtk = xc[k];
+      P.st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(P.rs);
+      P.lm = lam[k] + P.gk;                                 // dL/dQ_t (+ dL/dout[:, t])
+      const R gx = (P.xtk >= cs.qlb) ? P.lm : R(0);         // clamp backward (inclusive)
+      P.gb64 = (double)gx + (double)A[k];                   // (I - C1 N)^T gb = gx (utils.py:188-242)
+      P.gb = R(P.gb64);
+      P.Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);              // Q_{t-1}
+    };
+    auto adjoint = [&](int k, const Pre& P, AdjOutR<R>& o) {
       if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
-        const AdjOut o = adjoint_step_fast(st, Qp, cs, gb, xtk, Sx, I);
-        c1 = o.c1; c2 = o.c2; c3 = o.c3; c4 = o.c4; gQ = o.gQ; gn = o.gn; gq = o.gq; gp = o.gp;
+        const AdjOut f = adjoint_step_fast(P.st, P.Qp, cs, P.gb, P.xtk, P.Sx, P.I);
+        o = AdjOutR<R>{f.c1, f.c2, f.c3, f.c4, f.gQ, f.gn, f.gq, f.gp};
       } else {
-        const R qvk = *qs_at<R>(a, B, xs_base, tau, off_of(k), rs);  // q'[t-1] * flow_scale
+        const R qvk = *qs_at<R>(a, B, xs_base, tau, off_of(k), P.rs);  // q'[t-1] * flow_scale
         R tw, ss;
         Geom<R> geo;
-        coefficients<R, !DDR_BWD_EXACT>(st, Qp, cs, c1, c2, c3, c4, tw, ss, &geo);
+        coefficients<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, o.c1, o.c2, o.c3, o.c4, tw, ss, &geo);
         const R qc = rmax(qvk, cs.qlb);
-        const R gc1 = gb * Sx, gc2 = gb * I, gc3 = gb * Qp, gc4 = gb * qc;
-        coefficients_vjp<R, !DDR_BWD_EXACT>(st, Qp, cs, geo, c1, c2, c3, c4, gc1, gc2, gc3, gc4, gQ, gn, gq, gp);
+        const R gc1 = P.gb * P.Sx, gc2 = P.gb * P.I, gc3 = P.gb * P.Qp, gc4 = P.gb * qc;
+        coefficients_vjp<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, geo, o.c1, o.c2, o.c3, o.c4, gc1, gc2, gc3, gc4, o.gQ, o.gn,
+                                            o.gq, o.gp);
       }
-      if (active) {
-        pn[k] = pn[k] + gn;
-        pq[k] = pq[k] + gq;
-        pp[k] = pp[k] + gp;
+    };
+    auto post = [&](int k, const Pre& P, const AdjOutR<R>& o) {
+      const int r = P.r, t = P.t;
+      const R gb = P.gb;
+      if (P.active) {
+        pn[k] = pn[k] + o.gn;
+        pq[k] = pq[k] + o.gq;
+        pp[k] = pp[k] + o.gp;
         // flush the fp32 partial sums into the fp64 accumulators every kGradFlush *steps* (aligned to
         // t, not to ticks, so the summation grouping -- and the result -- is independent of the
         // partition); one owner per address, so the atomics are deterministic
@@ -1384,16 +1416,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           atomicAdd(g3p + 2, (double)pp[k]);
           pn[k] = pq[k] = pp[k] = R(0);
         }
-        saw[r] = R((double)c1 * gb64);
-        sbw[r] = c2 * gb;
-        lam[k] = ((gb * c3) + gQ) + Bd[k];
+        saw[r] = R((double)o.c1 * P.gb64);
+        sbw[r] = o.c2 * gb;
+        lam[k] = ((gb * o.c3) + o.gQ) + Bd[k];
         // dL/dqc = gb c4 (b = ... + c4 qc), through qc = clamp(q' * flow_scale) (mmc.py:421-424)
-        if constexpr (GS) gqs[xs_base + (int64_t)tau * B.nloc + r] = (qsv[k] >= cs.qlb) ? gb * c4 : R(0);
-      } else if (!kSt && GS && hk && t == 0) {
+        if constexpr (GS) gqs[xs_base + (int64_t)tau * B.nloc + r] = (qsv[k] >= cs.qlb) ? gb * o.c4 : R(0);
+      } else if (!kSt && GS && P.hk && t == 0) {
         if (carry) {
           // Q0 = q0 feeds step 1 unclamped; runoff[:, 0] = clamp(q0) per reach, or the gauge sum's clamp
           // (already folded into gk through gmask0)
-          if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = a.g_roff ? lm : lam[k] + ((xtk >= cs.qlb) ? gk : R(0));
+          if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = a.g_roff ? P.lm : lam[k] + ((P.xtk >= cs.qlb) ? P.gk : R(0));
           gqs[xs_base + (int64_t)tau * B.nloc + r] = R(0);
           saw[r] = R(0);
           sbw[r] = R(0);
@@ -1404,17 +1436,48 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           sbw[r] = R(0);
         }
       }
-      }  // wave_act
+    };
+    auto tail = [&](int k, const Pre& P) {
       if constexpr (GS) {
         const int tn = tau > 0 ? tau - 1 : 0;  // the next backward tick's row
-        qsv[k] = *qs_at<R>(a, B, xs_base, tn, off_of(k), rs);
+        qsv[k] = *qs_at<R>(a, B, xs_base, tn, off_of(k), P.rs);
       }
       // dL/drunoff of the next step's group, one tick ahead
-      const int tn = t - 1;
-      if (hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
+      const int tn = P.t - 1;
+      if (P.hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
         const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3), kGReg ? opq(gsg[kGReg ? k : 0]) : -1);
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
+    };
+#pragma unroll
+    for (int k0 = 0; k0 < KR; k0 += NPB) {
+      if (wbase + k0 * BS >= B.nloc) continue;
+      Pre P[NPB];
+#pragma unroll
+      for (int h = 0; h < NPB; ++h) pre(k0 + h, P[h]);
+      // the step's adjoint only where some lane of the wave runs a step this tick (DDR_SKIP_IDLE_BWD)
+      bool any = false;
+#pragma unroll
+      for (int h = 0; h < NPB; ++h) any = any || P[h].active || (GS && P[h].hk && P[h].t == 0);
+      const bool wave_act = !DDR_SKIP_IDLE_BWD || __builtin_amdgcn_ballot_w64(any) != 0;
+      if (wave_act) {
+        AdjOutR<R> o[NPB];
+        if constexpr (NPB == 2) {
+          // two slices' adjoint steps in packed halves (the same bits as two scalar steps)
+          AdjOut f0, f1;
+          adjoint_step_fast2(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].xtk, P[0].Sx, P[0].I},
+                             AdjIn{P[1].Qp, P[1].gb, P[1].xtk, P[1].Sx, P[1].I}, cs, f0, f1);
+          o[0] = AdjOutR<R>{f0.c1, f0.c2, f0.c3, f0.c4, f0.gQ, f0.gn, f0.gq, f0.gp};
+          o[1] = AdjOutR<R>{f1.c1, f1.c2, f1.c3, f1.c4, f1.gQ, f1.gn, f1.gq, f1.gp};
+        } else {
+#pragma unroll
+          for (int h = 0; h < NPB; ++h) adjoint(k0 + h, P[h], o[h]);
+        }
+#pragma unroll
+        for (int h = 0; h < NPB; ++h) post(k0 + h, P[h], o[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < NPB; ++h) tail(k0 + h, P[h]);
       __builtin_amdgcn_sched_barrier(0);
     }
     phz.mark(4);  // loads issue + compute
@@ -1986,6 +2049,15 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
     if (gsel && g->max_nloc <= 256) return launch(gather_qprime_kernel<R, 32, 256>, 32, 256);
     if (gsel && g->max_nloc <= 512) return launch(gather_qprime_kernel<R, 32, 512>, 32, 512);
     if (gsel && g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
+  }
+  if constexpr (sizeof(R) == 4) {
+    static const int heavy_g = [] {
+      const char* v = getenv("DDR_GATHER_HEAVY_G");
+      return v ? atoi(v) : 0;
+    }();
+    if (heavy_g == 4) return launch(gather_qprime_kernel<R, 4, 1024>, 4, 1024);
+    if (heavy_g == 2) return launch(gather_qprime_kernel<R, 2, 1024>, 2, 1024);
+    if (heavy_g == 16 && g->max_nloc <= 2048) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
   }
   return launch(gather_qprime_kernel<R, G, 1024>, G, 1024);
 }
