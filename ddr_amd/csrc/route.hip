@@ -2050,15 +2050,6 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
     if (gsel && g->max_nloc <= 512) return launch(gather_qprime_kernel<R, 32, 512>, 32, 512);
     if (gsel && g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
   }
-  if constexpr (sizeof(R) == 4) {
-    static const int heavy_g = [] {
-      const char* v = getenv("DDR_GATHER_HEAVY_G");
-      return v ? atoi(v) : 0;
-    }();
-    if (heavy_g == 4) return launch(gather_qprime_kernel<R, 4, 1024>, 4, 1024);
-    if (heavy_g == 2) return launch(gather_qprime_kernel<R, 2, 1024>, 2, 1024);
-    if (heavy_g == 16 && g->max_nloc <= 2048) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
-  }
   return launch(gather_qprime_kernel<R, G, 1024>, G, 1024);
 }
 
