@@ -417,7 +417,9 @@ __device__ __forceinline__ const R* qs_at(const RouteArgs& a, const BlockDesc& B
 // thread's slices run their physics in lockstep.
 // MATH: 0 exact (reference op order, correctly rounded pow), 1 fast (DDR_FWD_FAST_MATH), 2 faithful
 // (DDR_FWD_FAITHFUL_MATH: exact op order and IEEE divisions, fp32 faithful-class pow).
-template <typename R, int KR, int MATH>
+// XB: the x slots' buffer count when not the KR rule's (fwd_xbuf): 2 = parity-indexed slots and one barrier
+// per tick at KR = 4 too, where the launch finds the LDS for them (launch_route_kr)
+template <typename R, int KR, int MATH, int XB = 0>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
 #ifndef DDR_FWD_NP
@@ -446,7 +448,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // kDbl: [2][S] x slots by tick parity -- tick tau reads buffer (tau - 1) & 1 and writes its results
   // straight into buffer tau & 1, one workgroup barrier per tick; else [S], written in a publish phase
   // between two barriers
-  constexpr int kXBuf = fwd_xbuf(KR);
+  constexpr int kXBuf = XB > 0 ? XB : fwd_xbuf(KR);
   constexpr bool kDbl = kXBuf == 2;
   double* sx = reinterpret_cast<double*>(smem + kMathTabBytes);         // [kXBuf][S] x_j(t), solve precision
   const StatTab<R> tab{reinterpret_cast<R*>(sx + kXBuf * S)};           // [S][6]
@@ -1903,13 +1905,32 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
                        (const double*)(a.bwd_bnd + 2 * g->n_cut * a.T), (R*)a.gn, (R*)a.gq, (R*)a.gp);
   } else {
     auto kern = route_forward_kernel<R, KR, 0>;
+    size_t fsmem = smem;
     if constexpr (std::is_same<R, float>::value) {
       if (a.flags & DDR_FWD_FAST_MATH) kern = route_forward_kernel<R, KR, 1>;
       else if (a.flags & DDR_FWD_FAITHFUL_MATH) kern = route_forward_kernel<R, KR, 2>;
+      // KR = 4 (faithful): double-buffered x slots -- one barrier per tick -- where this graph's largest
+      // block leaves the LDS for a second buffer (C5's blocks of <= ~3800 reaches; C3's 4096 do not)
+      if constexpr (KR == 4) {
+        static const bool dbl4 = [] {
+          const char* v = getenv("DDR_FWD_DBL4");
+          return v == nullptr || atoi(v) != 0;
+        }();
+        const size_t b2 = route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt,
+                                          (size_t)g->max_cout, (size_t)g->max_xl, false, sizeof(R), g->kr, 2);
+        const size_t s2 = align16(b2) + split_table_bytes(g, false);
+        if (dbl4 && (a.flags & DDR_FWD_FAITHFUL_MATH) && s2 <= kLdsBudget) {
+          kern = route_forward_kernel<R, KR, 2, 2>;
+          fsmem = s2;
+          a.xl_off = (int32_t)(b2 - (size_t)g->max_xl * 4);
+          a.own_off = a.xl_off - (int32_t)align16(4 * (size_t)std::max(g->max_virt, g->max_cout));
+          a.xt_off = g->split.nranks > 0 ? (int32_t)align16(b2) : 0;
+        }
+      }
     }
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)fsmem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
+    hipLaunchKernelGGL(kern, grid, block, fsmem, stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     if (a.q_last || a.tw_last || a.ss_last) {

@@ -31,7 +31,7 @@ def consts_of(case):
 
 
 def run_hip(case, dev, dtype=torch.float32, gkw=None, gauges=None, q0=None, qprime=None, W=None, grads=True,
-            graph=None):
+            graph=None, math="exact"):
     """Reference recipe on the device: denormalize in torch, fused route, backward(W)."""
     rng = case.params["parameter_ranges"]
     ls = case.params["log_space_parameters"]
@@ -45,7 +45,7 @@ def run_hip(case, dev, dtype=torch.float32, gkw=None, gauges=None, q0=None, qpri
     g = graph if graph is not None else RiverGraph(case.n, case.rows, case.cols, **(gkw or {}))
     qp = tt(case.qprime if qprime is None else qprime)
     runoff, q_last, tw, ss = route(g, qp, n, q, p, tt(case.length), slope, tt(case.x), gauges=gauges,
-                                   q0=None if q0 is None else tt(q0), consts=consts_of(case))
+                                   q0=None if q0 is None else tt(q0), consts=consts_of(case), math=math)
     out = {"runoff": runoff.detach().cpu().numpy(), "q_last": q_last.detach().cpu().numpy(),
            "top_width": tw.detach().cpu().numpy(), "side_slope": ss.detach().cpu().numpy(), "graph": g}
     # the exact physical inputs the kernel saw (torch's device expf in the log-space denormalize may
@@ -144,6 +144,23 @@ def test_partition_invariance_and_determinism(cuda):
         np.testing.assert_array_equal(alt["runoff"], base["runoff"])
         for k in ("grad_n", "grad_q_spatial", "grad_p_spatial"):
             np.testing.assert_array_equal(alt[k], base[k])
+
+
+def test_faithful_partition_invariance_with_full_workgroups(cuda):
+    """The faithful forward (the drop-in default) is bitwise partition-invariant too, including blocks of
+    more than 2048 reaches (KR = 4, whose x slots are double-buffered when the LDS allows) against one
+    reach per thread (KR = 1, storer waves) and two (KR = 2)."""
+    net = synthetic.forest(synthetic.zipf_sizes(30000, 60, 0.4), seed=12, single_inflow=0.35)
+    case = synthetic_case(net, 120, 12)
+    big = run_hip(case, cuda, gkw={"target_blocks": 8}, math="faithful")
+    assert big["graph"].info.reaches_per_thread == 4 and big["graph"].info.n_cut > 0
+    for gkw in ({"max_block_reaches": 500, "target_blocks": 1 << 20}, {"max_block_reaches": 1500, "target_blocks": 1 << 20}):
+        alt = run_hip(case, cuda, gkw=gkw, math="faithful")
+        assert alt["graph"].info.reaches_per_thread in (1, 2)
+        np.testing.assert_array_equal(alt["runoff"], big["runoff"])
+        np.testing.assert_array_equal(alt["q_last"], big["q_last"])
+        for k in ("grad_n", "grad_q_spatial", "grad_p_spatial"):
+            np.testing.assert_array_equal(alt[k], big[k])
 
 
 def test_basin_independence(cuda):

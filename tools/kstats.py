@@ -1,10 +1,16 @@
 """Per-kernel duration summary from a rocprofv3 rocpd database (kernel trace).
-Usage: python tools/kstats.py DB [DB...] [--limit N]"""
+Usage: python tools/kstats.py DB [DB...] [--limit N] [--full] [--per-step K]
+--full prints whole kernel names; --per-step K adds the per-step total (total / K)."""
 import sqlite3
 import sys
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 limit = 40
+full = "--full" in sys.argv
+per_step = 0
+if "--per-step" in sys.argv:
+    per_step = int(sys.argv[sys.argv.index("--per-step") + 1])
+    args = [a for a in args if a != str(per_step)]
 if "--limit" in sys.argv:
     limit = int(sys.argv[sys.argv.index("--limit") + 1])
     args = [a for a in args if a != str(limit)]
@@ -17,6 +23,8 @@ for db in args:
     tot = 0.0
     for name, n, avg, mn, mx, t in c.execute(q):
         tot += t
-        print(f"{name[:60]:60s} {n:4d} {avg:10.3f} {mn:10.3f} {mx:10.3f} {t:10.3f}")
+        nm = name if full else f"{name[:60]:60s}"
+        ps = f" {t / per_step:10.3f}" if per_step else ""
+        print(f"{nm} {n:4d} {avg:10.3f} {mn:10.3f} {mx:10.3f} {t:10.3f}{ps}")
     n_all, t_all = c.execute("select count(*), sum(end-start)/1e6 from kernels").fetchone()
     print(f"all kernels: {n_all} dispatches, {t_all:.3f} ms")
