@@ -89,12 +89,49 @@ __global__ void k_jump(int64_t n, const int32_t* p, const int32_t* d, int32_t* p
   d2[i] = d[i] + d[q];
 }
 
+// Wave-aggregated atomics on keyed counters: the lanes sharing the first active lane's key combine their
+// values (one wave reduction) and that lane issues one atomic; repeated for up to kAggRounds distinct keys,
+// the rest atomically per lane.  Reaches of one basin / piece are mostly numbered together, so a wave
+// holds one or two keys: ~1M same-address atomics per build (0.4-0.5 ms each for basin sizes and the
+// piece table at C3) become a few per wave.
+constexpr int kAggRounds = 4;
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+// op 0: add, 1: max
+template <int OP>
+__device__ __forceinline__ void wave_atomic(int32_t* base, int32_t key, int32_t val, bool active) {
+  const int lane = threadIdx.x & 63;
+  for (int r = 0; r < kAggRounds; ++r) {
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(active);
+    if (m == 0) return;
+    const int leader = __builtin_ffsll((long long)m) - 1;
+    const int32_t k = __builtin_amdgcn_readlane(key, leader);
+    const bool mine = active && key == k;
+    const int32_t agg = OP == 0 ? wave_sum_i(mine ? val : 0) : wave_max_i(mine ? val : INT32_MIN);
+    if (lane == leader) {
+      if (OP == 0) atomicAdd(base + k, agg);
+      else atomicMax(base + k, agg);
+    }
+    active = active && !mine;
+  }
+  if (active) {
+    if (OP == 0) atomicAdd(base + key, val);
+    else atomicMax(base + key, val);
+  }
+}
+
 // basin sizes, deepest reach, outlet count
 __global__ void k_stats(int64_t n, const int32_t* down, const int32_t* basin, const int32_t* dist, int32_t* bsize,
                         int32_t* agg) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = i < n;
-  if (in) atomicAdd(bsize + basin[i], 1);
+  wave_atomic<0>(bsize, in ? basin[i] : 0, 1, in);
   // the graph-wide maximum depth and outlet count: one atomic per wave, not per reach (a million
   // same-address atomics serialised to ~0.5 ms per build)
   int dmax = in ? dist[i] : 0;
@@ -171,6 +208,124 @@ __global__ void __launch_bounds__(256) k_sub_ht(const int32_t* roots, const int3
   }
 }
 
+// Level order position of every reach, and the child table in level order: cnt[p] children of reach
+// ord[p], cpos[p] the level positions of its first four (column order; -1 past the count)
+__global__ void k_inv(int64_t n, const int32_t* ord, int32_t* inv) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) inv[ord[p]] = (int32_t)p;
+}
+__global__ void k_child_tab(int64_t n, const int32_t* ord, const int32_t* crow, const int32_t* col, const int32_t* inv,
+                            int32_t* cnt, int4* cpos) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t i = ord[p], k0 = crow[i], k1 = crow[i + 1];
+  cnt[p] = k1 - k0;
+  int4 q;
+  q.x = k0 + 0 < k1 ? inv[col[k0 + 0]] : -1;
+  q.y = k0 + 1 < k1 ? inv[col[k0 + 1]] : -1;
+  q.z = k0 + 2 < k1 ? inv[col[k0 + 2]] : -1;
+  q.w = k0 + 3 < k1 ? inv[col[k0 + 3]] : -1;
+  cpos[p] = q;
+}
+
+__device__ __forceinline__ void lds_barrier_dg() {
+  // LDS hand-off only: global loads issued ahead stay in flight across the barrier
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// k_sub_ht with the basin's subtree sizes and heights in LDS (segments of at most kLevelLds reaches;
+// larger basins take the global walk of k_sub_ht): a level reads its children's values from LDS at
+// positions from the child table, whose rows (and the level bounds) are requested a level ahead -- a
+// level costs an LDS round trip and a barrier instead of a chain of four dependent global loads
+constexpr int kLevelLds = 20480;  // reaches: 4 B size + 2 B height each, 120 KB
+__global__ void __launch_bounds__(256) k_sub_ht_lds(const int32_t* roots, const int32_t* nroots, const int32_t* seg_lo,
+                                                    const int32_t* seg_hi, const int32_t* lvl_next, const int32_t* ord,
+                                                    const int32_t* crow, const int32_t* col, const int32_t* inv,
+                                                    const int32_t* cnt, const int4* cpos, int32_t* sub, int32_t* ht) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lsm[];
+  int32_t* sub_l = reinterpret_cast<int32_t*>(lsm);
+  uint16_t* ht_l = reinterpret_cast<uint16_t*>(lsm + 4 * kLevelLds);
+  const int tid = threadIdx.x;
+  for (int32_t b = blockIdx.x; b < *nroots; b += gridDim.x) {
+    const int32_t root = roots[b];
+    const int32_t lo = seg_lo[root], hi = seg_hi[root];
+    if (hi - lo > kLevelLds) {
+      // the global walk (k_sub_ht's body)
+      for (int32_t s = lo; s < hi;) {
+        const int32_t e = lvl_next[s];
+        for (int32_t p = s + tid; p < e; p += blockDim.x) {
+          const int32_t i = ord[p];
+          int32_t su = 1, h = 0;
+          for (int32_t k = crow[i]; k < crow[i + 1]; ++k) {
+            const int32_t c = col[k];
+            su += sub[c];
+            h = max(h, ht[c] + 1);
+          }
+          sub[i] = su;
+          ht[i] = h;
+        }
+        __threadfence_block();
+        __syncthreads();
+        s = e;
+      }
+      continue;
+    }
+    int32_t s = lo, e = lvl_next[lo];
+    int32_t e2 = e < hi ? lvl_next[e] : hi;
+    int32_t pc = 0;
+    int4 pq = make_int4(-1, -1, -1, -1);
+    if (s + tid < e) {
+      pc = cnt[s + tid];
+      pq = cpos[s + tid];
+    }
+    while (s < hi) {
+      // the next level's first row and the level after's bound, requested before this level's work
+      int32_t nc = 0;
+      int4 nq = make_int4(-1, -1, -1, -1);
+      if (e + tid < e2) {
+        nc = cnt[e + tid];
+        nq = cpos[e + tid];
+      }
+      const int32_t e3 = e2 < hi ? lvl_next[e2] : hi;
+      for (int32_t p = s + tid; p < e; p += blockDim.x) {
+        int32_t c4 = pc;
+        int4 q = pq;
+        if (p != s + tid) {
+          c4 = cnt[p];
+          q = cpos[p];
+        }
+        int32_t su = 1, h = 0;
+        auto add = [&](int32_t cp) {
+          su += sub_l[cp - lo];
+          h = max(h, (int32_t)ht_l[cp - lo] + 1);
+        };
+        if (c4 > 0) add(q.x);
+        if (c4 > 1) add(q.y);
+        if (c4 > 2) add(q.z);
+        if (c4 > 3) add(q.w);
+        if (c4 > 4) {
+          const int32_t i = ord[p], k0 = crow[i];
+          for (int32_t k = k0 + 4; k < k0 + c4; ++k) add(inv[col[k]]);
+        }
+        sub_l[p - lo] = su;
+        ht_l[p - lo] = (uint16_t)h;
+      }
+      lds_barrier_dg();
+      s = e;
+      e = e2;
+      e2 = e3;
+      pc = nc;
+      pq = nq;
+    }
+    for (int32_t p = lo + tid; p < hi; p += blockDim.x) {
+      const int32_t i = ord[p];
+      sub[i] = sub_l[p - lo];
+      ht[i] = ht_l[p - lo];
+    }
+    __syncthreads();  // (the next basin reuses the LDS)
+  }
+}
+
 // Stem-preserving split of the basins larger than scap (graph.cpp build_graph, same rule and the
 // same tie-breaks: the deepest child by (height, size), first in column order; the others by
 // ascending residual size, ties in column order).  Smaller basins stay one piece.
@@ -238,6 +393,156 @@ __global__ void __launch_bounds__(256) k_split(const int32_t* roots, const int32
   }
   }
 }
+// Per level position, everything the split reads that no level writes (k_sub_ht's sizes and heights):
+// a = (own size, own height, child count, 0), and per child j < 4 (column order) its level position,
+// reach, size and height -- one coalesced row per position for k_split_lds
+struct SplitRow {
+  int4 a, pos, id, sz, h;
+};
+__global__ void k_split_tab(int64_t n, const int32_t* ord, const int32_t* cnt, const int4* cpos, const int32_t* sub,
+                            const int32_t* ht, SplitRow* tab) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int32_t i = ord[p], c = cnt[p];
+  SplitRow r;
+  r.a = make_int4(sub[i], ht[i], c, 0);
+  r.pos = cpos[p];
+  const int32_t q[4] = {r.pos.x, r.pos.y, r.pos.z, r.pos.w};
+  int32_t id[4], sz[4], hh[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    id[j] = j < c ? ord[q[j]] : -1;
+    sz[j] = j < c ? sub[id[j]] : 0;
+    hh[j] = j < c ? ht[id[j]] : 0;
+  }
+  r.id = make_int4(id[0], id[1], id[2], id[3]);
+  r.sz = make_int4(sz[0], sz[1], sz[2], sz[3]);
+  r.h = make_int4(hh[0], hh[1], hh[2], hh[3]);
+  tab[p] = r;
+}
+
+// k_split with the residual sizes and stem lengths of a basin in LDS (segments of at most kLevelLds
+// reaches; larger basins take k_split's global walk) and every static input from the split table,
+// requested a level ahead: the same decisions in the same order (deepest child by (height, size),
+// first in column order; the others by ascending (residual, column position))
+__global__ void __launch_bounds__(256) k_split_lds(const int32_t* roots, const int32_t* nroots, const int32_t* seg_lo,
+                                                   const int32_t* seg_hi, const int32_t* lvl_next, const int32_t* ord,
+                                                   const int32_t* crow, const int32_t* col, const int32_t* inv,
+                                                   const SplitRow* tab, const int32_t* sub, const int32_t* ht,
+                                                   int32_t* resid, int32_t* stem, uint8_t* is_root, int64_t scap_arg,
+                                                   const int32_t* agg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lsm[];
+  int32_t* res_l = reinterpret_cast<int32_t*>(lsm);
+  uint16_t* stem_l = reinterpret_cast<uint16_t*>(lsm + 4 * kLevelLds);
+  const int64_t scap = scap_arg >= 0 ? scap_arg : (int64_t)agg[3];
+  const int64_t lseg = scap / 8;
+  const int tid = threadIdx.x;
+  for (int32_t bb = blockIdx.x; bb < *nroots; bb += gridDim.x) {
+    const int32_t root = roots[bb];
+    if (sub[root] <= scap) continue;
+    const int32_t lo = seg_lo[root], hi = seg_hi[root];
+    const bool in_lds = hi - lo <= kLevelLds;
+    // a reach's residual / stem: LDS (by level position) or global (by reach)
+    auto get_res = [&](int32_t pos, int32_t id) { return in_lds ? res_l[pos - lo] : resid[id]; };
+    auto get_stem = [&](int32_t pos, int32_t id) { return in_lds ? (int32_t)stem_l[pos - lo] : stem[id]; };
+    auto put = [&](int32_t p, int32_t i, int32_t r, int32_t st) {
+      if (in_lds) {
+        res_l[p - lo] = r;
+        stem_l[p - lo] = (uint16_t)st;
+      } else {
+        resid[i] = r;
+        stem[i] = st;
+      }
+    };
+    // one position: the split rule of k_split
+    auto step = [&](int32_t p, const SplitRow& R) {
+      const int32_t i = ord[p];
+      const int32_t nc = R.a.z;
+      if ((int64_t)R.a.x <= scap || nc == 0) {
+        put(p, i, R.a.x, R.a.y + 1);
+        return;
+      }
+      // children j < nc: (position, reach, size, height); beyond 4 from the CSR
+      auto child = [&](int32_t j, int32_t& pos, int32_t& id, int32_t& sz, int32_t& h) {
+        if (j < 4) {
+          pos = j == 0 ? R.pos.x : j == 1 ? R.pos.y : j == 2 ? R.pos.z : R.pos.w;
+          id = j == 0 ? R.id.x : j == 1 ? R.id.y : j == 2 ? R.id.z : R.id.w;
+          sz = j == 0 ? R.sz.x : j == 1 ? R.sz.y : j == 2 ? R.sz.z : R.sz.w;
+          h = j == 0 ? R.h.x : j == 1 ? R.h.y : j == 2 ? R.h.z : R.h.w;
+        } else {
+          id = col[crow[i] + j];
+          pos = inv[id];
+          sz = sub[id];
+          h = ht[id];
+        }
+      };
+      int32_t dj = 0, dpos, did, dsz, dh;
+      child(0, dpos, did, dsz, dh);
+      for (int32_t j = 1; j < nc; ++j) {
+        int32_t cp, ci, cs, ch;
+        child(j, cp, ci, cs, ch);
+        if (ch > dh || (ch == dh && cs > dsz)) {
+          dj = j; dpos = cp; did = ci; dsz = cs; dh = ch;
+        }
+      }
+      const int32_t dres = get_res(dpos, did), dstem = get_stem(dpos, did);
+      int64_t base = 1 + (int64_t)dres, trib = (int64_t)dres - dstem;
+      const bool keep = base <= scap;
+      if (!keep) {
+        is_root[did] = 1;
+        base = 1;
+        trib = 0;
+      }
+      int64_t acc = 0;
+      // the other children in (resid, column position) order: a selection per step (few children)
+      int64_t pr = -1, pk = -1;
+      for (int32_t stp = 0; stp < nc - 1; ++stp) {
+        int64_t br = 0x7fffffffffffffffll, bk = -1;
+        int32_t bid = -1;
+        for (int32_t j = 0; j < nc; ++j) {
+          if (j == dj) continue;
+          int32_t cp, ci, cs, ch;
+          child(j, cp, ci, cs, ch);
+          const int64_t r = get_res(cp, ci);
+          const bool after = r > pr || (r == pr && j > pk);
+          if (after && (r < br || (r == br && j < bk))) {
+            br = r;
+            bk = j;
+            bid = ci;
+          }
+        }
+        if (trib + acc + br <= scap - lseg && base + acc + br <= scap) acc += br;
+        else is_root[bid] = 1;
+        pr = br;
+        pk = bk;
+      }
+      put(p, i, (int32_t)(base + acc), keep ? 1 + dstem : 1);
+    };
+    int32_t s = lo, e = lvl_next[lo];
+    int32_t e2 = e < hi ? lvl_next[e] : hi;
+    SplitRow pr0{};
+    if (s + tid < e) pr0 = tab[s + tid];
+    while (s < hi) {
+      SplitRow nr{};
+      if (e + tid < e2) nr = tab[e + tid];
+      const int32_t e3 = e2 < hi ? lvl_next[e2] : hi;
+      for (int32_t p = s + tid; p < e; p += blockDim.x) step(p, p == s + tid ? pr0 : tab[p]);
+      if (in_lds) {
+        lds_barrier_dg();
+      } else {
+        __threadfence_block();
+        __syncthreads();
+      }
+      s = e;
+      e = e2;
+      e2 = e3;
+      pr0 = nr;
+    }
+    // (resid / stem are read by this kernel only: the LDS copies are not written back)
+    __syncthreads();  // (the next basin reuses the LDS)
+  }
+}
+
 // the first pass's split threshold (graph.cpp plan_init: cap x 100 % without a dominant basin, 80 % with
 // one), from the largest basin -- so the host reads the statistics only with the first piece table
 __global__ void k_scap(int64_t n, int64_t cap, int32_t pct_override, int32_t* agg) {
@@ -265,12 +570,13 @@ __global__ void k_piece_table(int64_t n, const int32_t* down, const uint8_t* is_
                               const int32_t* dloc, const int32_t* crow, const int32_t* ht, const int32_t* dist,
                               int32_t* tab) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t p = piece[i];
-  atomicAdd(tab + 1 * n + p, 1);
-  atomicMax(tab + 2 * n + p, dloc[i]);
-  const int32_t deg = crow[i + 1] - crow[i];
-  if (deg > 2) atomicAdd(tab + 3 * n + p, deg);
+  const bool in = i < n;
+  const int32_t p = in ? piece[i] : 0;
+  wave_atomic<0>(tab + 1 * n, p, 1, in);
+  wave_atomic<1>(tab + 2 * n, p, in ? dloc[i] : 0, in);
+  const int32_t deg = in ? crow[i + 1] - crow[i] : 0;
+  wave_atomic<0>(tab + 3 * n, p, deg, in && deg > 2);
+  if (!in) return;
   if (is_root[i]) {
     const int32_t d = down[i];
     tab[0 * n + p] = (int32_t)i;
@@ -551,6 +857,9 @@ struct DevBuild {
   int32_t *basin = nullptr, *dist = nullptr, *ord = nullptr, *seg_lo = nullptr, *seg_hi = nullptr, *lvl_next = nullptr;
   int32_t *roots = nullptr, *sub = nullptr, *ht = nullptr, *resid = nullptr, *stem = nullptr, *pflag = nullptr;
   int32_t *prank = nullptr, *q = nullptr, *dloc = nullptr, *piece = nullptr, *tab = nullptr;
+  int32_t* inv = nullptr;            // level position of every reach (level walks in LDS)
+  SplitRow* split_tab = nullptr;     // the split's static inputs per level position (k_split_lds)
+  bool level_lds = true;
   uint8_t* is_root = nullptr;
   unsigned basin_grid = 1;
   // host side of the piece-table reads: pinned, so the copies are truly asynchronous
@@ -673,8 +982,27 @@ struct DevBuild {
     if ((st = exclusive_sum<int32_t>(scr, oflag, orank, n, s))) return st;
     hipLaunchKernelGGL(k_roots, dim3(nblk(n)), dim3(kTB), 0, s, n, down, orank, roots);
     basin_grid = (unsigned)std::min<int64_t>(n, 8192);  // workgroups striding over the basins
-    hipLaunchKernelGGL(k_sub_ht, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
-                       kids, sub, ht);
+    {
+      const char* v = getenv("DDR_DEVBUILD_LEVEL_LDS");
+      level_lds = v == nullptr || atoi(v) != 0;
+    }
+    if (level_lds) {
+      inv = scr.get<int32_t>(n);
+      int32_t* ccnt = scr.get<int32_t>(n);
+      int4* cpos = scr.get<int4>(n);
+      split_tab = scr.get<SplitRow>(n);
+      DDR_SCR(inv); DDR_SCR(ccnt); DDR_SCR(cpos); DDR_SCR(split_tab);
+      hipLaunchKernelGGL(k_inv, dim3(nblk(n)), dim3(kTB), 0, s, n, ord, inv);
+      hipLaunchKernelGGL(k_child_tab, dim3(nblk(n)), dim3(kTB), 0, s, n, ord, crow, kids, inv, ccnt, cpos);
+      const int lds = kLevelLds * 6;
+      DDR_HIP(hipFuncSetAttribute((const void*)k_sub_ht_lds, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      hipLaunchKernelGGL(k_sub_ht_lds, dim3(basin_grid), dim3(256), lds, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord,
+                         crow, kids, inv, ccnt, cpos, sub, ht);
+      hipLaunchKernelGGL(k_split_tab, dim3(nblk(n)), dim3(kTB), 0, s, n, ord, ccnt, cpos, sub, ht, split_tab);
+    } else {
+      hipLaunchKernelGGL(k_sub_ht, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
+                         kids, sub, ht);
+    }
     DDR_HIP(hipGetLastError());
     phase("sub+ht", tp);
     // ---- the first split pass (its threshold chosen on the device from the largest basin) -----
@@ -710,8 +1038,15 @@ struct DevBuild {
   ddr_status pass() {
     ddr_status st;
     DDR_HIP(hipMemsetAsync(is_root, 0, n, s));
-    hipLaunchKernelGGL(k_split, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
-                       kids, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
+    if (level_lds) {
+      const int lds = kLevelLds * 6;
+      DDR_HIP(hipFuncSetAttribute((const void*)k_split_lds, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+      hipLaunchKernelGGL(k_split_lds, dim3(basin_grid), dim3(256), lds, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord,
+                         crow, kids, inv, split_tab, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
+    } else {
+      hipLaunchKernelGGL(k_split, dim3(basin_grid), dim3(256), 0, s, roots, agg + 1, seg_lo, seg_hi, lvl_next, ord, crow,
+                         kids, sub, ht, resid, stem, is_root, first ? int64_t(-1) : plan.scap(), agg);
+    }
     hipLaunchKernelGGL(k_piece_flags, dim3(nblk(n)), dim3(kTB), 0, s, n, down, is_root, pflag);
     DDR_HIP(hipGetLastError());
     DDR_HIP(hipMemsetAsync(pflag + n, 0, 4, s));  // prank[n] = number of pieces
