@@ -1121,6 +1121,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if (tid == 0) sx[S - 1] = R(0);
   if (kDbl && tid == 0) sx[2 * S - 1] = R(0);
   const bool vown = tid < B.nvirt;
+  // Import waves (KR = 1, blocks whose reaches, virtuals and chunk imports each fit half the workgroup):
+  // the upper half's idle waves run the cut-out imports in a loop of their own, requesting each chunk's
+  // granules DDR_BWD_IMP_EARLY ticks before its boundary tick, so the routing waves' import phase shrinks
+  // to the barrier that hands the ring over
+#ifndef DDR_BWD_IMPWAVES
+#define DDR_BWD_IMPWAVES 1
+#endif
+#ifndef DDR_BWD_IMP_EARLY
+#define DDR_BWD_IMP_EARLY 4
+#endif
+  static_assert(DDR_BWD_IMP_EARLY >= 0 && DDR_BWD_IMP_EARLY < kChunkBwd, "import lead within a chunk");
+  const bool imp_mode = KR == 1 && kDbl && DDR_BWD_IMPWAVES && !(a.flags & kFlagNoStorer) && B.ncout > 0 &&
+                        B.nloc <= BS / 2 && B.nvirt <= BS / 2 && B.ncout * kChunkBwd <= BS / 2;
   // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
   // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
   // tid < ncout: its import owner)
@@ -1271,7 +1284,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // cut edge of cut-out c is B.cout0 + c (graph.cpp numbers cut edges in block order), its tick
       // offset is in the owner words
       const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
-      for (int w = tid; w < B.ncout * kChunkBwd; w += BS) {
+      for (int w = tid; !imp_mode && w < B.ncout * kChunkBwd; w += BS) {
         const int c = w / kChunkBwd, sidx = w % kChunkBwd;
         const int t = (tau - sidx) - (int)(own[c] >> 16);
         R A = R(0), Bv = R(0);
@@ -1546,6 +1559,58 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1);
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
+  if (imp_mode && wbase >= BS / 2) {
+    // import waves: thread w owns (cut-out w / kChunkBwd, step slot w % kChunkBwd) of every chunk; per tick
+    // the same barriers as the routing waves' tick (the ring hand-off at a chunk boundary, the tick's end)
+    const int w = tid - BS / 2;
+    const bool wown = w < B.ncout * kChunkBwd;
+    const int c = wown ? w / kChunkBwd : 0, sidx = w % kChunkBwd;
+    const uintptr_t p = !wown ? 0 : a.xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
+    const bool sys = p & 1u;
+    const double* prow = reinterpret_cast<const double*>(p & ~uintptr_t(1));
+    const int coff = wown ? (int)(own[c] >> 16) : 0;
+    auto step_of = [&](int tb) { return (TT - 1 - tb - sidx) - coff; };  // the step chunk tb's slot needs
+    unsigned long long eg[2] = {0ull, 0ull};
+    bool issued = false;
+#pragma unroll 1
+    for (int tb = 0; tb < TT; ++tb) {
+      if ((tb % kChunkBwd) == 0) {
+        if (wown) {
+          const int t = step_of(tb);
+          R A = R(0), Bv = R(0);
+          if (t >= tmin && t < T) {
+            double g[2];
+            const double* row = prow + (int64_t)t * 2;
+            if (issued) {
+              if (sys) poll_granules<2, true>(row, 0, 0, 2, eg, g, a.status, bid, force_to);
+              else poll_granules<2, false>(row, 0, 0, 2, eg, g, a.status, bid, force_to);
+            } else {
+              if (sys) wait_granules<2, true>(row, 0, 1, 0, 2, g, a.status, bid, force_to);
+              else wait_granules<2>(row, 0, 1, 0, 2, g, a.status, bid, force_to);
+            }
+            A = R(g[0]);
+            Bv = R(g[1]);
+          }
+          ring[(c * kChunkBwd + sidx) * 2] = A;
+          ring[(c * kChunkBwd + sidx) * 2 + 1] = Bv;
+        }
+        issued = false;
+        lds_barrier();
+      }
+      const int nb = tb + DDR_BWD_IMP_EARLY;
+      if (DDR_BWD_IMP_EARLY > 0 && wown && (nb % kChunkBwd) == 0 && nb < TT) {
+        const int t = step_of(nb);
+        if (t >= tmin && t < T) {
+          const double* row = prow + (int64_t)t * 2;
+          if (sys) issue_granules<2, true>(row, 0, 0, 2, eg);
+          else issue_granules<2, false>(row, 0, 0, 2, eg);
+          issued = true;
+        }
+      }
+      lds_barrier();  // the routing waves' tick end
+    }
+    return;
+  }
   phz.start();
   using Gen = std::integral_constant<bool, false>;
   using Steady = std::integral_constant<bool, true>;
