@@ -68,14 +68,19 @@ def test_steady_path_gauge_mode(cuda):
 
 @pytest.mark.parametrize("T", [300, 302], ids=["rows16B", "ragged"])
 def test_storer_waves_are_bitwise_the_compute_wave_stores(cuda, T):
-    """Light blocks (<= 512 reaches, one per thread) store x_save / runoff from their idle upper waves;
-    outputs and gradients equal the compute-wave stores bit for bit (T % 4 != 0: per-step runoff stores)."""
+    """Light blocks (<= 512 reaches, one per thread) store x_save / runoff from their idle upper waves in
+    the forward, and import the cut-outs' (A, B) granules on them in the backward (requested ahead of the
+    chunk boundary); outputs and gradients equal the compute-wave stores and imports bit for bit (T % 4 != 0:
+    per-step runoff stores)."""
     net = synthetic.forest(synthetic.loguniform_sizes(12, 50, 3000, 11), seed=11)
     case = synthetic_case(net, T, 11)
     g = RiverGraph(net.n, net.rows, net.cols, max_block_reaches=256, target_blocks=1 << 20)
     assert g.info.reaches_per_thread == 1
+    assert g.info.n_cut > 0  # cut edges: the backward imports run
     q0 = np.random.default_rng(12).uniform(0.1, 5.0, net.n).astype(np.float32)
-    for kw in ({}, {"q0": q0}):
+    outlets = np.flatnonzero(net.down < 0)
+    gz = GaugeMap.build([np.array([o]) for o in outlets], net.n, cuda)
+    for kw in ({}, {"q0": q0}, {"gauges": gz}):
         a = _run(case, cuda, g, "faithful", flags=0, **kw)
         b = _run(case, cuda, g, "faithful", flags=_lib.DDR_DEBUG_NO_STORER, **kw)
         for k in a:
