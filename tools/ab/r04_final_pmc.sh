@@ -2,7 +2,7 @@
 # Round-4 evidence, PMC part: tools/pmc.sh passes (one counter group per pass) for the given workloads,
 # turned into counter files keyed to the loaded library's build (tools/pmc_to_json.py, written under
 # gpurun_out/TAG/counters/ -> profiles/counters/), plus the readable reports.
-# Usage: bash tools/r04_final_pmc.sh TAG c5 [c3 c4 c2]
+# Usage: bash tools/ab/r04_final_pmc.sh TAG c5 [c3 c4 c2]
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
