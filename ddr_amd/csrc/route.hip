@@ -1132,8 +1132,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #define DDR_BWD_IMP_EARLY 4
 #endif
   static_assert(DDR_BWD_IMP_EARLY >= 0 && DDR_BWD_IMP_EARLY < kChunkBwd, "import lead within a chunk");
-  const bool imp_mode = KR == 1 && kDbl && DDR_BWD_IMPWAVES && !(a.flags & kFlagNoStorer) && B.ncout > 0 &&
-                        B.nloc <= BS / 2 && B.nvirt <= BS / 2 && B.ncout * kChunkBwd <= BS / 2;
+  const bool help_ok = KR == 1 && kDbl && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2 && B.nvirt <= BS / 2 &&
+                       B.ncout * kChunkBwd <= BS / 2;
+  const bool imp_mode = help_ok && DDR_BWD_IMPWAVES && B.ncout > 0;
+  // x helpers (same blocks): the upper half also loads each reach's x(t - 4) row from x_save, DDR_BWD_XHELP_D
+  // ticks ahead, and publishes it into the reach's slot, so the routing waves issue no x_save load and do
+  // not wait at the tick's top for one
+#ifndef DDR_BWD_XHELP
+#define DDR_BWD_XHELP 1
+#endif
+#ifndef DDR_BWD_XHELP_D
+#define DDR_BWD_XHELP_D 3
+#endif
+  const bool xhelp = help_ok && DDR_BWD_XHELP;
   // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
   // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
   // tid < ncout: its import owner)
@@ -1276,7 +1287,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     R* sxw = sx + (kDbl ? ((tb + 1) & 1) * S : 0);        // (kDbl) x published for the next tick
     if constexpr (kEarly) {
       constexpr int ahead = kDbl ? 1 : 0;
-      load_own(tau - 3 - ahead, xbn, tq);                          // x(t - 3) (kDbl: x(t - 4)), published next tick
+      if (!xhelp) load_own(tau - 3 - ahead, xbn, tq);              // x(t - 3) (kDbl: x(t - 4)), published next tick
       if (vown) vxn = load_virt((int64_t)tau - 1 - ahead - v_off - 2);  // the virtual's value for the next tick
     }
     if (B.ncout > 0 && (tb % kChunkBwd) == 0) {
@@ -1331,7 +1342,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (wbase + k * BS >= B.nloc) continue;
       const int r = tq + k * BS;
       // x(t - 2): the upstream value of the downstream reach's step t - 1 (kDbl: next tick's, x(t - 3))
-      if (r < B.nloc) sxw[r] = xbc[k];
+      if (!xhelp && r < B.nloc) sxw[r] = xbc[k];
       const int dl = dl_of(k);
       if (dl >= 0) {
         A[k] = sar[dl];
@@ -1496,16 +1507,22 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       __builtin_amdgcn_sched_barrier(0);
     }
     phz.mark(4);  // loads issue + compute
+    // next tick: x(t - 1) -> x(t); x(t - 2), still in the own slot -> x(t - 1).  kDbl: read before the
+    // barrier (no one writes this tick's read buffer during the tick; after the barrier the x helpers
+    // may already be writing it for the next tick)
+    auto shift_x = [&]() {
+#pragma unroll
+      for (int k = 0; k < KR; ++k) {
+        if (wbase + k * BS >= B.nloc) continue;
+        const int r = tq + k * BS;
+        xc[k] = xa[k];
+        xa[k] = r < B.nloc ? sxr[r] : R(0);
+      }
+    };
+    if constexpr (kDbl) shift_x();
     lds_barrier();
     phz.mark(5);  // barrier 2
-    // next tick: x(t - 1) -> x(t); x(t - 2), still in the own slot -> x(t - 1)
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      if (wbase + k * BS >= B.nloc) continue;
-      const int r = tq + k * BS;
-      xc[k] = xa[k];
-      xa[k] = r < B.nloc ? sxr[r] : R(0);
-    }
+    if constexpr (!kDbl) shift_x();
   };
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2, x(t-2) at row TT-3
@@ -1559,11 +1576,24 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1);
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
-  if (imp_mode && wbase >= BS / 2) {
+  if ((imp_mode || xhelp) && wbase >= BS / 2) {
     // import waves: thread w owns (cut-out w / kChunkBwd, step slot w % kChunkBwd) of every chunk; per tick
-    // the same barriers as the routing waves' tick (the ring hand-off at a chunk boundary, the tick's end)
+    // the same barriers as the routing waves' tick (the ring hand-off at a chunk boundary, the tick's end).
+    // x helpers: thread w < nloc publishes reach w's x(t - 4) (forward row TT - 4 - tb at tick tb, clamped)
+    // into the next tick's x buffer, its loads issued DDR_BWD_XHELP_D ticks ahead
     const int w = tid - BS / 2;
-    const bool wown = w < B.ncout * kChunkBwd;
+    const bool wown = imp_mode && w < B.ncout * kChunkBwd;
+    const bool xown = xhelp && w < B.nloc;
+    constexpr int XD = DDR_BWD_XHELP_D;
+    const R* xcol = xsave + xs_base + (xown ? w : 0);
+    auto xload = [&](int tb) -> R {
+      int tc = TT - 4 - tb;
+      tc = tc < 0 ? 0 : (tc >= TT ? TT - 1 : tc);
+      return xown ? xcol[(int64_t)tc * B.nloc] : R(0);
+    };
+    R xp[XD];
+#pragma unroll
+    for (int i = 0; i < XD; ++i) xp[i] = xload(i);
     const int c = wown ? w / kChunkBwd : 0, sidx = w % kChunkBwd;
     const uintptr_t p = !wown ? 0 : a.xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
     const bool sys = p & 1u;
@@ -1572,9 +1602,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     auto step_of = [&](int tb) { return (TT - 1 - tb - sidx) - coff; };  // the step chunk tb's slot needs
     unsigned long long eg[2] = {0ull, 0ull};
     bool issued = false;
-#pragma unroll 1
-    for (int tb = 0; tb < TT; ++tb) {
-      if ((tb % kChunkBwd) == 0) {
+    auto htick = [&](int tb, R& xr) {
+      if (B.ncout > 0 && (tb % kChunkBwd) == 0) {
         if (wown) {
           const int t = step_of(tb);
           R A = R(0), Bv = R(0);
@@ -1597,6 +1626,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         issued = false;
         lds_barrier();
       }
+      if (xown) {
+        sx[((tb + 1) & 1) * S + w] = xr;  // the routing waves read it next tick
+        xr = xload(tb + XD);
+      }
       const int nb = tb + DDR_BWD_IMP_EARLY;
       if (DDR_BWD_IMP_EARLY > 0 && wown && (nb % kChunkBwd) == 0 && nb < TT) {
         const int t = step_of(nb);
@@ -1608,6 +1641,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         }
       }
       lds_barrier();  // the routing waves' tick end
+    };
+    // unrolled by XD: each prefetch register is consumed in place (a register copy would wait for its load)
+#pragma unroll 1
+    for (int tb = 0; tb < TT; tb += XD) {
+#pragma unroll
+      for (int i = 0; i < XD; ++i)
+        if (tb + i < TT) htick(tb + i, xp[i]);
     }
     return;
   }

@@ -70,8 +70,8 @@ def test_steady_path_gauge_mode(cuda):
 def test_storer_waves_are_bitwise_the_compute_wave_stores(cuda, T):
     """Light blocks (<= 512 reaches, one per thread) store x_save / runoff from their idle upper waves in
     the forward, and import the cut-outs' (A, B) granules on them in the backward (requested ahead of the
-    chunk boundary); outputs and gradients equal the compute-wave stores and imports bit for bit (T % 4 != 0:
-    per-step runoff stores)."""
+    chunk boundary) and publish each reach's x(t - 4) from x_save ahead of time; outputs and gradients equal
+    the compute-wave stores, imports and x loads bit for bit (T % 4 != 0: per-step runoff stores)."""
     net = synthetic.forest(synthetic.loguniform_sizes(12, 50, 3000, 11), seed=11)
     case = synthetic_case(net, T, 11)
     g = RiverGraph(net.n, net.rows, net.cols, max_block_reaches=256, target_blocks=1 << 20)
