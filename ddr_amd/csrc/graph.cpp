@@ -262,6 +262,13 @@ ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* ou
   double maxfac = 1.0;
   for (double f : fac) maxfac = std::max(maxfac, f);
   const double capw0 = wsum / (double)limit;
+  // light loads (capacity <= half a workgroup, one reach per thread): no block above half a workgroup while
+  // the capacity stays there -- a block of 513+ reaches has no idle upper waves (storer / import / x-helper
+  // waves, route.hip) and three routing waves per SIMD, and sets the kernel's pace (a C3 8-way shard's
+  // five 700-reach blocks: 8.15 ms against 6.9-7.5 for the shards without); the capacity growth below
+  // lifts the clamp when the blocks do not fit otherwise
+  const bool light_clamp = !getenv("DDR_PACK_NO_LIGHT_CLAMP") && P.cap <= kBlockThreads / 2;
+  const double bc_max = light_clamp ? (double)(kBlockThreads / 2) : (double)P.hard_cap;
   auto pack = [&](int k) {
     const double capw = capw0 * std::pow(1.01, (double)k);
     load.clear();
@@ -280,7 +287,7 @@ ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* ou
       if (best < 0) {
         best = (int64_t)load.size();
         load.push_back(0);
-        double bc = std::min<double>((double)P.hard_cap, std::max<double>((double)sz, capw / fac[p]));
+        double bc = std::min<double>(bc_max, std::max<double>((double)sz, capw / fac[p]));
         if (P.pack_quant > 1 && bc >= (double)P.pack_quant)
           bc = std::max<double>((double)sz, std::floor(bc / (double)P.pack_quant) * (double)P.pack_quant);
         bcap.push_back(bc);
@@ -347,7 +354,15 @@ ddr_status pack_pieces(PackPlan& P, const PieceTable& pt, PackResult& R, int* ou
   if (ncut > 0 && nblocks > limit) {
     *outcome = kPackResplit;
     if (P.cap < P.hard_cap) {
-      P.cap = std::min<int64_t>(P.hard_cap, P.cap + P.cap / 32 + 1);
+      const int64_t grown = std::min<int64_t>(P.hard_cap, P.cap + P.cap / 32 + 1);
+      // light loads: before the capacity leaves half a workgroup (blocks of 513+ reaches lose their idle
+      // waves, see light_clamp), the unweighted packing at this capacity (C3 8-way shard 3: 7.72 ms with
+      // one 530-reach block, 7.35 ms unweighted at 512, 8.16 ms before the clamp; profiles/r04/ab_r04.txt)
+      if (light_clamp && P.weighted && grown > kBlockThreads / 2) {
+        P.weighted = false;
+        return DDR_OK;
+      }
+      P.cap = grown;
       return DDR_OK;
     }
     if (P.weighted) {
