@@ -193,3 +193,24 @@ def test_generation_fallback_builds_fast():
     g2 = host_graph(net.n, net.rows, net.cols, steps_hint=2136, max_resident=180, target_blocks=180)
     assert time.perf_counter() - t < 5.0
     assert g2.info.generations == 2 and g2.info.n_blocks <= 360
+
+
+def test_light_load_blocks_keep_half_a_workgroup(monkeypatch):
+    """At light load (block capacity <= 512 reaches, one per thread) no block exceeds 512 reaches: a larger
+    one loses the idle helper waves and runs three routing waves per SIMD (route.hip).  C3 8-way shard 3
+    packed five ~700-reach blocks before the rule (graph.cpp light_clamp; profiles/r04/ab_r04.txt item 24);
+    DDR_PACK_NO_LIGHT_CLAMP restores the previous packing, which the last assertion checks is still the
+    case that needs the rule."""
+    from ddr_amd.distributed import shard_network
+
+    net = synthetic.forest(synthetic.loguniform_sizes(256, 100, 20000, 3), seed=3, single_inflow=0.25)
+    for r in (1, 3):
+        n, rows, cols, _ = shard_network(net.n, net.rows, net.cols, r, 8)
+        g = host_graph(n, rows, cols, steps_hint=2136)
+        nl = np.bincount(g.structure()["block"], minlength=g.info.n_blocks)
+        assert g.info.reaches_per_thread == 1 and g.info.generations == 1
+        assert nl.max() <= 512, (r, int(nl.max()))
+        assert g.info.n_blocks <= 256
+    monkeypatch.setenv("DDR_PACK_NO_LIGHT_CLAMP", "1")
+    g = host_graph(n, rows, cols, steps_hint=2136)
+    assert np.bincount(g.structure()["block"]).max() > 512
