@@ -67,6 +67,25 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Wave priority by remaining slices (DDR_SLICE_PRIO): the SIMD's arbiter serves its oldest ready wave
+// first, so the workgroup's first waves finish their slices early and the youngest runs its last slices
+// alone at the end of every tick, one dependent chain issuing on the SIMD.  A wave at slice k of KR takes
+// priority KR - 1 - k (the top of the tick: 3), so the waves with more work left go first and the
+// SIMD's waves finish together.  KR = 4 (full load): C5 129.4 -> 126.2 ms, C3 forward 16.0 -> 14.4 ms
+// (profiles/r04/ab_r04.txt item 28); at KR = 2 no gain was measured (C4), KR = 1 has one slice.
+#ifndef DDR_SLICE_PRIO
+#define DDR_SLICE_PRIO 1
+#endif
+__device__ __forceinline__ void set_prio(int p) {
+  if (!DDR_SLICE_PRIO) return;
+  switch (p) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+}
+
 __device__ __forceinline__ void store_granule(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -686,6 +705,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // it wait again, vmcnt(0), at the first use of qcur -- after this tick's prefetch was issued)
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
+    if constexpr (KR == 4) set_prio(3);
     phz.mark(0);  // the previous tick's loads and stores
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
@@ -711,6 +731,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k0 = 0; k0 < KR; k0 += NP) {
       if (wbase + k0 * BS >= B.nloc) continue;
+      if constexpr (KR == 4) set_prio(KR - 1 - k0);
       if (!kSt && DDR_SKIP_IDLE) {
         // no lane of the wave runs a step this tick (before its first / after its last step: the
         // first and last dmax ticks of a block, most ticks of a short window): skip the slice
@@ -1269,6 +1290,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // conservative count across the divergent load branches waits (vmcnt(0)) at the first use of a
     // previous-tick register, i.e. for the loads issued in THIS tick too.
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    if constexpr (KR == 4) set_prio(3);
     phz.mark(0);  // the previous tick's loads and stores
     const int tq = opq(tid);
 #pragma unroll
@@ -1478,6 +1500,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int k0 = 0; k0 < KR; k0 += NPB) {
       if (wbase + k0 * BS >= B.nloc) continue;
+      if constexpr (KR == 4) set_prio(KR - 1 - k0);
       Pre P[NPB];
 #pragma unroll
       for (int h = 0; h < NPB; ++h) pre(k0 + h, P[h]);
