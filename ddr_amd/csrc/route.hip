@@ -76,6 +76,13 @@ __device__ __forceinline__ void lds_barrier() {
 #ifndef DDR_SLICE_PRIO
 #define DDR_SLICE_PRIO 1
 #endif
+// (DDR_LIGHT_PRIO, forward at KR = 1) a routing wave runs its step's physics at priority 1 and the rest at 0:
+// of the two routing waves on a SIMD, the one ahead yields once its physics is done, so the two finish
+// together (c3s8 forward 2.87 -> 2.75 ms; C2 and c5s8r5 within noise; the backward's adjoint showed no
+// change; profiles/r04/ab_r04.txt item 30)
+#ifndef DDR_LIGHT_PRIO
+#define DDR_LIGHT_PRIO 1
+#endif
 __device__ __forceinline__ void set_prio(int p) {
   if (!DDR_SLICE_PRIO) return;
   switch (p) {
@@ -706,6 +713,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
     if constexpr (KR == 4) set_prio(3);
+    if constexpr (KR == 1 && DDR_LIGHT_PRIO) __builtin_amdgcn_s_setprio(1);
     phz.mark(0);  // the previous tick's loads and stores
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
@@ -780,6 +788,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
         for (int h = 0; h < NP; ++h) ph[h] = PhysOut<R>{R(0), R(0), R(0), R(0), R(0), R(0)};
       }
+      if constexpr (KR == 1 && DDR_LIGHT_PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
         const int k = k0 + h;
