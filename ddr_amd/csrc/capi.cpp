@@ -126,29 +126,55 @@ struct PendingStatus {
   }
 } g_pending;
 
-// DDR_FWD_CHECK_QPRIME: per host thread, the NaN word of its last checked forward, copied to pinned memory
-// behind the q' gather, and the event after that copy (ddr_qprime_nan_wait waits for the gather only)
+// Restores the calling thread's current device on scope exit (entry points that act on a graph's own
+// device, which need not be the caller's current one)
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t error = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    error = hipGetDevice(&prev);
+    if (error == hipSuccess && prev != dev) error = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// DDR_FWD_CHECK_QPRIME: per host thread and device, the NaN word of its last checked forward, copied to
+// pinned memory behind the q' gather, and the event after that copy (ddr_qprime_nan_wait waits for the
+// gather only).  Keyed by device: an event belongs to the device current at its creation, so a thread
+// routing on several GPUs records each launch's event on that launch's own device
+constexpr int kNanDevices = 64;
 struct NanCheck {
   unsigned* host = nullptr;
   hipEvent_t ev = nullptr;
   bool armed = false;
 };
-thread_local NanCheck t_nan;
+thread_local NanCheck t_nan[kNanDevices];
+thread_local int t_nan_dev = -1;  // device of the calling thread's last checked forward
 
 hipError_t nan_check_mark(const void* status, hipStream_t s) {
-  if (!t_nan.host) {
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&t_nan.host), 16, hipHostMallocDefault);
-    if (e != hipSuccess) return e;
-  }
-  if (!t_nan.ev) {
-    hipError_t e = hipEventCreateWithFlags(&t_nan.ev, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-  }
-  hipError_t e = hipMemcpyAsync(t_nan.host, static_cast<const unsigned*>(status) + kStatusNaN, sizeof(unsigned),
-                                hipMemcpyDeviceToHost, s);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  t_nan.armed = true;
-  return hipEventRecord(t_nan.ev, s);
+  if (dev < 0 || dev >= kNanDevices) return hipErrorInvalidDevice;
+  NanCheck& c = t_nan[dev];
+  if (!c.host) {
+    e = hipHostMalloc(reinterpret_cast<void**>(&c.host), 16, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+  }
+  if (!c.ev) {
+    e = hipEventCreateWithFlags(&c.ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  e = hipMemcpyAsync(c.host, static_cast<const unsigned*>(status) + kStatusNaN, sizeof(unsigned),
+                     hipMemcpyDeviceToHost, s);
+  if (e != hipSuccess) return e;
+  if (t_nan_dev >= 0) t_nan[t_nan_dev].armed = false;  // "the last checked forward" is this one
+  c.armed = true;
+  t_nan_dev = dev;
+  return hipEventRecord(c.ev, s);
 }
 
 hipError_t timing_mark(int which, int edge, hipStream_t s) {
@@ -322,7 +348,8 @@ template <typename R>
 ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_mc_reaches* r, const R* qprime,
                          int64_t T, const R* x_save, const double* bnd, const R* grad, const ddr_gauges* gauges,
                          double* bwd_bnd, void* status, R* gn, R* gq, R* gp, int32_t flags, void* stream,
-                         int64_t qp_rows = 0, R* gqp = nullptr, R* gq0 = nullptr, void* work = nullptr) {
+                         int64_t qp_rows = 0, R* gqp = nullptr, R* gq0 = nullptr, void* work = nullptr,
+                         const R* seed = nullptr) {
   ddr_status st = check_common<R>(gh, c, r, T);
   if (st) return st;
   const Graph* g = reinterpret_cast<const Graph*>(gh);
@@ -358,6 +385,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   a.grad_out = grad;
   a.g_roff = gauges ? gauges->reach_offsets : nullptr;
   a.g_rg = gauges ? gauges->reach_gauges : nullptr;
+  a.gseed = seed;
   a.bwd_bnd = bwd_bnd;
   a.gn = gn;
   a.gq = gq;
@@ -457,6 +485,21 @@ ddr_status gauge_daily_seed_impl(int64_t G, int64_t T, int64_t t0, int64_t L, in
   } catch (...) {                                        \
     return fail(DDR_ERR_ARG, "internal error");          \
   }
+
+template <typename R>
+ddr_status state_impl(const ddr_graph* gh, const R* x_save, int64_t T, int64_t t, double qlb, int32_t flags, R* out,
+                      void* stream) {
+  if (!gh || !x_save || !out) return fail(DDR_ERR_ARG, "null state argument");
+  const Graph* g = reinterpret_cast<const Graph*>(gh);
+  if (!g->uploaded) return fail(DDR_ERR_ARG, "graph was built host-only: upload it first (ddr_graph_upload)");
+  if (T < 1 || t < 0 || t >= T) return fail(DDR_ERR_ARG, "state step out of [0, T)");
+  // a split rank holds the states of its own blocks only
+  if (g->split.nranks > 0) return fail(DDR_ERR_ARG, "split basin: the saved states are per rank");
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DDR_HIP(graph_ready(g, s));
+  DDR_HIP(launch_state_at<R>(g, T, t, qlb, (flags & DDR_FWD_CARRY) != 0, x_save, out, s));
+  return DDR_OK;
+}
 
 extern "C" {
 
@@ -606,10 +649,15 @@ ddr_status ddr_graph_build_async(int64_t n, int64_t e, const int32_t* rows, cons
 ddr_status ddr_graph_destroy(ddr_graph* g) {
   DDR_GUARD({
     Graph* gr = reinterpret_cast<Graph*>(g);
+    if (!gr) return DDR_OK;
+    // on the graph's own device (the caller may have another one current): its sync, and the null stream
+    // the pool-release events are recorded on
+    DeviceGuard dg(gr->device);
+    if (dg.error != hipSuccess) return fail(DDR_ERR_HIP, hipGetErrorString(dg.error));
     // synchronous, as the header promises: the pooled blocks of a device-built graph go back to the pool
     // only once no launch on any stream can still read them (their release event is recorded on the null
     // stream, which does not order PyTorch's non-blocking streams)
-    if (gr && (gr->device_built || !gr->async_allocations.empty())) DDR_HIP(hipDeviceSynchronize());
+    if (gr->device_built || !gr->async_allocations.empty()) DDR_HIP(hipDeviceSynchronize());
     destroy_graph(gr);
     return DDR_OK;
   })
@@ -618,10 +666,11 @@ ddr_status ddr_graph_destroy(ddr_graph* g) {
 ddr_status ddr_qprime_nan_wait(int32_t* has_nan) {
   DDR_GUARD({
     if (!has_nan) return fail(DDR_ERR_ARG, "null has_nan");
-    if (!t_nan.armed) return fail(DDR_ERR_ARG, "no DDR_FWD_CHECK_QPRIME forward on this thread");
-    DDR_HIP(hipEventSynchronize(t_nan.ev));
-    *has_nan = *t_nan.host ? 1 : 0;
-    t_nan.armed = false;
+    if (t_nan_dev < 0 || !t_nan[t_nan_dev].armed) return fail(DDR_ERR_ARG, "no DDR_FWD_CHECK_QPRIME forward on this thread");
+    NanCheck& c = t_nan[t_nan_dev];
+    DDR_HIP(hipEventSynchronize(c.ev));
+    *has_nan = *c.host ? 1 : 0;
+    c.armed = false;
     return DDR_OK;
   })
 }
@@ -907,6 +956,31 @@ ddr_status ddr_mc_backward_state_f64(const ddr_graph* g, const ddr_mc_consts* c,
                                      void* status, double* gn, double* gq, double* gp, double* grad_qprime,
                                      double* grad_q0, void* work, int32_t flags, void* stream) {
   DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work); })
+}
+ddr_status ddr_mc_backward_ex_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                  const float* qprime, int64_t qprime_rows, int64_t T, const float* x_save,
+                                  const double* bnd, const float* grad, const ddr_gauges* gauges,
+                                  const float* state_seed, double* bwd_bnd, void* status, float* gn, float* gq,
+                                  float* gp, float* grad_qprime, float* grad_q0, void* work, int32_t flags,
+                                  void* stream) {
+  DDR_GUARD({ return backward_impl<float>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work, state_seed); })
+}
+ddr_status ddr_mc_backward_ex_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                  const double* qprime, int64_t qprime_rows, int64_t T, const double* x_save,
+                                  const double* bnd, const double* grad, const ddr_gauges* gauges,
+                                  const double* state_seed, double* bwd_bnd, void* status, double* gn, double* gq,
+                                  double* gp, double* grad_qprime, double* grad_q0, void* work, int32_t flags,
+                                  void* stream) {
+  DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work, state_seed); })
+}
+
+ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
+                         int32_t flags, float* out, void* stream) {
+  DDR_GUARD({ return state_impl<float>(g, x_save, T, t, discharge_lb, flags, out, stream); })
+}
+ddr_status ddr_state_f64(const ddr_graph* g, const double* x_save, int64_t T, int64_t t, double discharge_lb,
+                         int32_t flags, double* out, void* stream) {
+  DDR_GUARD({ return state_impl<double>(g, x_save, T, t, discharge_lb, flags, out, stream); })
 }
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T, const ddr_gauges* gz,
                                 double qlb, int32_t flags, float* out, void* stream) {

@@ -68,7 +68,6 @@ ddr_status upload_schedule_async(Graph* g, hipStream_t stream) {
     pinned_put(host, stream);
     return fail(DDR_ERR_HIP, "graph upload: out of device memory");
   }
-  g->staging = host;
   g->async_allocations.push_back(dev);
   size_t o = 0;
   auto place = [&](const void* src, size_t n, size_t elem) {
@@ -97,7 +96,12 @@ ddr_status upload_schedule_async(Graph* g, hipStream_t stream) {
   put(&D.block_of_pos, H.block_of_pos);
   put(&D.rs_loc, H.rs_loc);
   put(&D.rs_ref, H.rs_ref);
-  DDR_HIP(hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, stream));
+  const hipError_t ce = hipMemcpyAsync(dev, host, total, hipMemcpyHostToDevice, stream);
+  // the staging block goes back to the pool at once: its event (recorded on `stream` behind the copy)
+  // keeps it from reuse until the copy has read it -- a prefetcher holding many built graphs pins no host
+  // memory per graph
+  pinned_put(host, stream);
+  DDR_HIP(ce);
   if (!g->ready) DDR_HIP(hipEventCreateWithFlags(&g->ready, hipEventDisableTiming));
   DDR_HIP(hipEventRecord(g->ready, stream));
   DDR_HIP(hipGetDevice(&g->device));

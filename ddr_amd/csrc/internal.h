@@ -87,10 +87,11 @@ constexpr size_t kMathTabBytes = 3072;
 // kMaxConfluenceList int32 entries per block (13-bit offsets in the packed upstream word).
 constexpr int kMaxConfluenceList = 8191;
 __host__ __device__ inline size_t route_lds_bytes(size_t slots, size_t nvirt, size_t ncout, size_t nxl, bool backward,
-                                                  size_t rsize, int kr = 4, int fwd_xb = 0) {
-  // fwd_xb: the forward's x-slot buffers when not the KR rule's (the double-buffered KR = 4 variant)
-  const size_t base = backward ? slots * (3 * (size_t)bwd_xbuf(kr) + 6) * rsize
-                               : slots * (8 * (size_t)(fwd_xb > 0 ? fwd_xb : fwd_xbuf(kr)) + 6 * rsize);
+                                                  size_t rsize, int kr = 4, int xb = 0) {
+  // xb: the slot buffers when not the KR rule's (the forward's double-buffered KR = 4 variant; the
+  // backward's single-buffered fp64 KR = 2 variant, whose double buffer does not fit)
+  const size_t base = backward ? slots * (3 * (size_t)(xb > 0 ? xb : bwd_xbuf(kr)) + 6) * rsize
+                               : slots * (8 * (size_t)(xb > 0 ? xb : fwd_xbuf(kr)) + 6 * rsize);
   const size_t ring = backward ? ncout * kChunkBwd * 2 * rsize : nvirt * kChunkFwd * 8;
   // backward: per hand-off owner thread (tid < max(nvirt, ncout)) its virtual's downstream slot and
   // its cut-out's tick offset

@@ -1017,6 +1017,31 @@ __global__ void __launch_bounds__(256) route_last_kernel(RouteArgs a) {
   }
 }
 
+// Q(t) of every reach, in reference order, from a forward's saved states (ddr_state_f32/f64): clamp(x(t)),
+// the carried state at t = 0 unclamped (mmc.py:441, 557) -- e.g. Q(T - 2), the state the reported
+// geometry of the last step was computed from (mmc.py:161-162), for that geometry's VJP
+template <typename R>
+__global__ void state_at_kernel(DevSchedule s, int64_t N, int64_t T, int64_t t, R qlb, int carry, const R* xsave,
+                                R* out) {
+  const int64_t P = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (P >= N) return;
+  const BlockDesc B = s.blocks[s.block_of_pos[P]];
+  const R x = xsave[T * B.pos0 + B.pre_dn + (t + s.off[P]) * B.nloc + (P - B.pos0)];
+  out[s.ref[P]] = (t == 0 && carry) ? x : rmax_nan(x, qlb);
+}
+
+template <typename R>
+hipError_t launch_state_at(const Graph* g, int64_t T, int64_t t, double qlb, bool carry, const R* xsave, R* out,
+                           hipStream_t stream) {
+  if (g->n == 0) return hipSuccess;
+  hipLaunchKernelGGL(state_at_kernel<R>, dim3((unsigned)((g->n + 255) / 256)), dim3(256), 0, stream, g->dev, g->n, T, t,
+                     R(qlb), carry ? 1 : 0, xsave, out);
+  return hipGetLastError();
+}
+template hipError_t launch_state_at<float>(const Graph*, int64_t, int64_t, double, bool, const float*, float*, hipStream_t);
+template hipError_t launch_state_at<double>(const Graph*, int64_t, int64_t, double, bool, const double*, double*,
+                                            hipStream_t);
+
 // one reach-step's adjoint outputs: coefficients, dL/dQ_{t-1} and the parameter gradient terms
 template <typename R>
 struct AdjOutR {
@@ -1050,7 +1075,9 @@ __device__ __forceinline__ Grad4<R> make_grad4(R a, R b, R c, R d) { return Grad
 // GS (state gradients, DDR_BWD_GRAD_*): the sweep also runs step 0 -- the hot start's transposed solve
 // (c1 = 1) into dL/d(q' * flow_scale)[0], or dL/dQ0 of a carried state -- and writes dL/d(q' * flow_scale)
 // of every step (gb c4 [q' >= q_lb], mmc.py:421-424, 535-538) into gqs, the schedule layout of qs.
-template <typename R, int KR, bool GS>
+// XB: the slot buffers when not the KR rule's (bwd_xbuf): 1 = single-buffered slots where the double buffer
+// does not fit the LDS (fp64 at KR = 2, bwd_xb_of)
+template <typename R, int KR, bool GS, int XB = 0>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1066,7 +1093,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // tick before (the downstream's (c1 gb, c2 gb) in buffer (tb + 1) & 1, the upstream's x in buffer tb & 1)
   // and writes its own for the next tick into the other buffers: one workgroup barrier per tick.  Else
   // [S] each, a publish phase and a compute phase between two barriers.
-  constexpr int kXB = bwd_xbuf(KR);
+  constexpr int kXB = XB > 0 ? XB : bwd_xbuf(KR);
   constexpr bool kDbl = kXB == 2 && (DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR);
   R* sa = reinterpret_cast<R*>(smem + kMathTabBytes);  // [kXB][S] c1_i gb_i (transposed solve, rounded to R)
   R* sb = sa + kXB * S;                                 // [kXB][S] c2_i gb_i (adjoint of the inflow)
@@ -1124,7 +1151,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
-    const bool nograd = a.g_roff != nullptr && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]];
+    const bool nograd = a.g_roff != nullptr && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]] && a.gseed == nullptr;
     if constexpr (kGReg) {
       gsg[k] = -1;
       if (a.g_roff != nullptr && a.g_roff[ref[k] + 1] - a.g_roff[ref[k]] == 1) gsg[k] = (int)a.g_rg[a.g_roff[ref[k]]];
@@ -1235,7 +1262,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
   // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439)
-  auto load_grad = [&](int ref, int64_t base, int gs) {
+  auto load_grad_out = [&](int ref, int64_t base, int gs) {
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
     const int64_t i1 = base + 1 < T ? base + 1 : T - 1, i2 = base + 2 < T ? base + 2 : T - 1,
                   i3 = base + 3 < T ? base + 3 : T - 1;
@@ -1280,6 +1307,20 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     }
     return make_grad4(row[base], row[i1], row[i2], row[i3]);
+  };
+  // ... plus the state seeds of steps T - 1 and T - 2 (a.gseed; a scalar test per group otherwise)
+  auto load_grad = [&](int ref, int64_t base, int gs) {
+    Grad4<R> v = load_grad_out(ref, base, gs);
+    if (a.gseed != nullptr && base + 3 >= T - 2) {
+      const R* sd = static_cast<const R*>(a.gseed);
+      const R s1 = sd[ref], s2 = sd[a.N + ref];
+      auto add = [&](R& g, int64_t t) { g = g + (t == T - 1 ? s1 : (t == T - 2 ? s2 : R(0))); };
+      add(v.a, base);
+      add(v.b, base + 1);
+      add(v.c, base + 2);
+      add(v.d, base + 3);
+    }
+    return v;
   };
 
   // virtual inflow's x(t_v - 2), prefetched one tick ahead (kept as loaded: converting it would
@@ -2005,18 +2046,39 @@ __global__ void gauge_daily_seed_kernel(int64_t G, int64_t T, int64_t t0, int64_
 // ============================================================================================
 // Host launchers
 // ============================================================================================
-template <typename R>
-size_t route_smem_bytes(const Graph* g, bool backward) {
-  return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt, (size_t)g->max_cout,
-                         (size_t)g->max_xl, backward, sizeof(R), g->kr);
-}
-
 // Split basin: after the layout, each block's granule rows (tagged pointers, bit 0 = another rank's
 // memory: system scope): forward, its cut-outs' export rows; backward, its virtuals' export rows then
 // its cut-outs' import rows -- resolved once per launch, no dependent global load per hand-off
 size_t split_table_bytes(const Graph* g, bool backward) {
   if (g->split.nranks == 0) return 0;
   return 8 * (size_t)(backward ? g->max_virt + g->max_cout : g->max_cout);
+}
+
+// The backward's slot buffers on this graph: the KR rule's, unless its double buffer does not fit a CU's
+// LDS at this real size (fp64 at KR = 2: 96 B per slot, ~1.6K-reach blocks), then one -- two barriers per
+// tick instead of DDR_ERR_CAPACITY (the graph packer sizes blocks for the fp32 layouts)
+template <typename R>
+int bwd_xb_of(const Graph* g) {
+  if (bwd_xbuf(g->kr) == 1) return 1;
+  const size_t b2 = route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt,
+                                    (size_t)g->max_cout, (size_t)g->max_xl, true, sizeof(R), g->kr, 2);
+  return (sizeof(R) == 8 && g->kr == 2 && align16(b2) + split_table_bytes(g, true) > kLdsBudget) ? 1 : 2;
+}
+
+template <typename R>
+size_t route_smem_bytes(const Graph* g, bool backward) {
+  return route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt, (size_t)g->max_cout,
+                         (size_t)g->max_xl, backward, sizeof(R), g->kr, backward ? bwd_xb_of<R>(g) : 0);
+}
+
+// the backward kernel of this launch (state gradients: GS; single-buffered fp64 KR = 2 slots: bwd_xb_of)
+template <typename R, int KR>
+const void* backward_kernel_of(const Graph* g, bool gs) {
+  if constexpr (KR == 2 && sizeof(R) == 8) {
+    if (bwd_xb_of<R>(g) == 1)
+      return gs ? (const void*)route_backward_kernel<R, KR, true, 1> : (const void*)route_backward_kernel<R, KR, false, 1>;
+  }
+  return gs ? (const void*)route_backward_kernel<R, KR, true> : (const void*)route_backward_kernel<R, KR, false>;
 }
 
 template <typename R, int KR>
@@ -2031,10 +2093,12 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   a.xt_off = g->split.nranks > 0 ? (int32_t)align16(base) : 0;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
-    auto kern = a.gqs ? route_backward_kernel<R, KR, true> : route_backward_kernel<R, KR, false>;
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    const void* kern = backward_kernel_of<R, KR>(g, a.gqs != nullptr);
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, grid, block, smem, stream, a);
+    void* kargs[] = {&a};
+    e = hipLaunchKernel(kern, grid, block, kargs, smem, stream);
+    if (e != hipSuccess) return e;
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned fb = (unsigned)((g->n + 255) / 256);
@@ -2097,9 +2161,9 @@ int max_resident_blocks(const Graph* g, bool backward) {
   const size_t smem = align16(route_smem_bytes<R>(g, backward)) + split_table_bytes(g, backward);
   const void* f = nullptr;
   switch (g->kr) {
-    case 1: f = backward ? (const void*)route_backward_kernel<R, 1, false> : (const void*)route_forward_kernel<R, 1, 0>; break;
-    case 2: f = backward ? (const void*)route_backward_kernel<R, 2, false> : (const void*)route_forward_kernel<R, 2, 0>; break;
-    default: f = backward ? (const void*)route_backward_kernel<R, 4, false> : (const void*)route_forward_kernel<R, 4, 0>;
+    case 1: f = backward ? backward_kernel_of<R, 1>(g, false) : (const void*)route_forward_kernel<R, 1, 0>; break;
+    case 2: f = backward ? backward_kernel_of<R, 2>(g, false) : (const void*)route_forward_kernel<R, 2, 0>; break;
+    default: f = backward ? backward_kernel_of<R, 4>(g, false) : (const void*)route_forward_kernel<R, 4, 0>;
   }
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, kBlockThreads, smem) != hipSuccess) return -1;
   hipDeviceProp_t prop;

@@ -53,6 +53,10 @@ struct RouteArgs {
   void* gqs;
   void* gq0;
   const unsigned char* gmask0;
+  // per-reach state seeds (reference order, R), or null: [0, N) dL/dQ_{T-1} (the final discharge state,
+  // mmc.py:441), [N, 2N) dL/dQ_{T-2} (the state the reported geometry reads, mmc.py:161-162); added to
+  // dL/dout of those steps (gauge mode: every reach reads its gradient groups)
+  const void* gseed;
   unsigned long long* prof;  // debug per-workgroup profile (ddr_set_block_profile), or null
   // split basin (SplitState, internal.h; null when not split): logical blocks of other ranks are
   // skipped, cross-rank cut edges read this rank's receive rows and write the peer's
@@ -86,6 +90,10 @@ struct GaugeArgs {
 
 template <typename R>
 hipError_t launch_route(const Graph* g, const RouteArgs& a, bool backward, hipStream_t stream);
+// Q(t) of every reach (reference order) from a forward's saved states (route.hip: state_at_kernel)
+template <typename R>
+hipError_t launch_state_at(const Graph* g, int64_t T, int64_t t, double qlb, bool carry, const R* xsave, R* out,
+                           hipStream_t stream);
 // split basin: the epoch hand-shake before a routing launch (route.hip: split_barrier_kernel)
 struct SplitBarrierArgs {
   unsigned long long* mine;                  // this rank's epoch words ([2][kMaxSplitRanks])

@@ -194,12 +194,14 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
                       p: torch.Tensor, length: torch.Tensor, slope: torch.Tensor, x_storage: torch.Tensor,
                       flow_scale: torch.Tensor | None, x_save: torch.Tensor, bnd: torch.Tensor,
                       g_off: torch.Tensor | None, g_idx: torch.Tensor | None, r_off: torch.Tensor | None,
-                      r_g: torch.Tensor | None, qp_valid: torch.Tensor | None, graph_id: int, consts: list[float],
-                      flags: int, steps: int, qp_hours: int, daily: list[int], want_qprime: bool, want_q0: bool
+                      r_g: torch.Tensor | None, qp_valid: torch.Tensor | None, gseed: torch.Tensor | None,
+                      graph_id: int, consts: list[float], flags: int, steps: int, qp_hours: int, daily: list[int],
+                      want_qprime: bool, want_q0: bool
                       ) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
     """Returns per-reach (dL/dn, dL/dq_spatial, dL/dp_spatial), dL/dq' (shape of ``qprime``, or empty)
     and dL/dQ0 (N, carried state, or empty).  With ``daily`` the incoming gradient is dL/d(daily
-    series) (G, D): its pooling adjoint seeds the gauge-mode routing adjoint."""
+    series) (G, D): its pooling adjoint seeds the gauge-mode routing adjoint.  ``gseed`` (2, N): per-reach
+    gradients into the states Q_{T-1} (``_discharge_t``) and Q_{T-2} (the reported geometry's), or None."""
     g = _graph(graph_id)
     T, N = int(steps), qprime.shape[1]
     dev, dt = qprime.device, qprime.dtype
@@ -232,17 +234,25 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
     want_q0 = want_q0 and bool(flags & _lib.DDR_FWD_CARRY)
     gqp = torch.empty(qprime.shape if want_qprime else (0,), device=dev, dtype=dt)
     gq0 = torch.empty(N if want_q0 else 0, device=dev, dtype=dt)
-    if want_qprime or want_q0:
-        # state-gradient adjoint (route_backward_kernel<GS>): also the step-0 sweep and dL/dq'
-        G = grad_runoff.shape[0] if gz is not None else 0
-        work = torch.empty(int(lib.ddr_state_work_bytes(g.handle, T, G, 4 if f32 else 8)), device=dev,
-                           dtype=torch.uint8)
-        bwd = lib.ddr_mc_backward_state_f32 if f32 else lib.ddr_mc_backward_state_f64
+    if gseed is not None:
+        gseed = gseed.to(dtype=dt).contiguous()
+        if gseed.shape != (2, N):
+            raise ValueError("state seed must be (2, N)")
+    if want_qprime or want_q0 or gseed is not None:
+        # the general adjoint: state gradients (route_backward_kernel<GS>: also the step-0 sweep and dL/dq')
+        # and / or the per-reach state seeds
+        work = None
+        if want_qprime or want_q0:
+            G = grad_runoff.shape[0] if gz is not None else 0
+            work = torch.empty(int(lib.ddr_state_work_bytes(g.handle, T, G, 4 if f32 else 8)), device=dev,
+                               dtype=torch.uint8)
+        bwd = lib.ddr_mc_backward_ex_f32 if f32 else lib.ddr_mc_backward_ex_f64
         _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), int(qprime.shape[0]), T, x_save.data_ptr(),
                        bnd.data_ptr() if bnd.numel() else None, grad_runoff.data_ptr(),
-                       C.byref(gz) if gz is not None else None, bwd_bnd.data_ptr(), status.data_ptr(),
-                       gn.data_ptr(), gq.data_ptr(), gp.data_ptr(), gqp.data_ptr() if want_qprime else None,
-                       gq0.data_ptr() if want_q0 else None, work.data_ptr(), int(flags), stream))
+                       C.byref(gz) if gz is not None else None, _lib.ptr(gseed), bwd_bnd.data_ptr(),
+                       status.data_ptr(), gn.data_ptr(), gq.data_ptr(), gp.data_ptr(),
+                       gqp.data_ptr() if want_qprime else None, gq0.data_ptr() if want_q0 else None,
+                       _lib.ptr(work), int(flags), stream))
     else:
         bwd = lib.ddr_mc_backward_f32 if f32 else lib.ddr_mc_backward_f64
         _lib.check(bwd(g.handle, C.byref(c), C.byref(r), qprime.data_ptr(), T, x_save.data_ptr(),
@@ -256,7 +266,7 @@ def mc_route_backward(grad_runoff: torch.Tensor, qprime: torch.Tensor, n: torch.
 
 @mc_route_backward.register_fake
 def _(grad_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, g_off, g_idx, r_off, r_g,
-      qp_valid, graph_id, consts, flags, steps, qp_hours, daily, want_qprime, want_q0):
+      qp_valid, gseed, graph_id, consts, flags, steps, qp_hours, daily, want_qprime, want_q0):
     N = qprime.shape[1]
     want_q0 = want_q0 and bool(flags & _lib.DDR_FWD_CARRY)
     return (qprime.new_empty(N), qprime.new_empty(N), qprime.new_empty(N),
@@ -284,34 +294,83 @@ def _setup_context(ctx, inputs, output):
     ctx.set_materialize_grads(False)
 
 
+def state_at(graph: RiverGraph, x_save: torch.Tensor, steps: int, t: int, discharge_lb: float, flags: int
+             ) -> torch.Tensor:
+    """Q_t (N, reference order) from a forward's saved states (``ddr_state_f32``): max(x(t), q_lb), the
+    carried state at t = 0 unclamped -- the reference's ``_discharge_t`` after step t (mmc.py:441, 557)."""
+    out = torch.empty(graph.n, device=x_save.device, dtype=x_save.dtype)
+    lib = _lib.load()
+    fn = lib.ddr_state_f32 if x_save.dtype == torch.float32 else lib.ddr_state_f64
+    _lib.check(fn(graph.handle, x_save.data_ptr(), int(steps), int(t), float(discharge_lb), int(flags), out.data_ptr(),
+                  _lib.stream_ptr(x_save.device)))
+    return out
+
+
+def _geometry_vjp(ctx, n, q, p, slope, x_save, g_tw, g_ss):
+    """VJP of the reported top width / side slope (mmc.py:161-162): the power-law geometry of the last step,
+    computed from Q_{T-2} (trapezoidal.py:62-79), differentiated by PyTorch's autograd like the reference's.
+    Returns dL/dQ_{T-2} (the adjoint's second state seed) and the geometry's own (dL/dn, dL/dq, dL/dp)."""
+    from .geometry.trapezoidal import compute_trapezoidal_geometry
+
+    T = ctx.steps
+    carry = bool(ctx.flags & _lib.DDR_FWD_CARRY)
+    if T < 2 or ctx.flags & _lib.DDR_FWD_ACCUMULATE:
+        raise NotImplementedError("this launch reports no geometry (T < 2 or an accumulation launch)")
+    if T == 2 and carry:
+        # Q_0 is then the carried state itself, which the adjoint seeds through runoff[:, 0]'s clamp
+        raise NotImplementedError("geometry gradients of a 2-step carried window (use route_timestep's state)")
+    qprev = state_at(ctx.graph, x_save, T, T - 2, ctx.consts[1], ctx.flags)
+    with torch.enable_grad():
+        Qv = qprev.detach().requires_grad_(True)
+        nv, qv, pv = (t.detach().requires_grad_(True) for t in (n, q, p))
+        geo = compute_trapezoidal_geometry(nv, pv, qv, Qv, slope, depth_lb=ctx.consts[4],
+                                           bottom_width_lb=ctx.consts[5])
+        outs, gouts = [], []
+        for key, gv in (("top_width", g_tw), ("side_slope", g_ss)):
+            if gv is not None:
+                outs.append(geo[key].expand_as(gv))
+                gouts.append(gv)
+        gQ, gn, gq, gp = torch.autograd.grad(outs, (Qv, nv, qv, pv), gouts, allow_unused=True)
+    z = lambda g_, like: torch.zeros_like(like) if g_ is None else g_  # noqa: E731
+    return z(gQ, Qv), z(gn, n), z(gq, q), z(gp, p)
+
+
 def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
     (qprime, n, q, p, length, slope, x_storage, flow_scale, x_save, bnd, g_off, g_idx, r_off, r_g,
      qp_valid) = ctx.saved_tensors
-    if g_tw is not None or g_ss is not None:
-        if (g_tw is not None and bool(g_tw.ne(0).any())) or (g_ss is not None and bool(g_ss.ne(0).any())):
-            raise NotImplementedError("gradients through top_width/side_slope are not supported by ddrx::mc_route")
     T = ctx.steps
+    N = qprime.shape[1]
+    nz = lambda g_: g_ is not None and bool(g_.ne(0).any())  # noqa: E731
+    geo = nz(g_tw) or nz(g_ss)
+    # per-reach state seeds (ddr_mc_backward_ex): row 0 dL/dQ_{T-1} = dL/d_discharge_t (an autograd tensor in
+    # the reference in gauge mode too, mmc.py:433-441), row 1 dL/dQ_{T-2} from the reported geometry's VJP
+    gseed = None
+    if g_qlast is not None or geo:
+        gseed = torch.zeros((2, N), device=qprime.device, dtype=qprime.dtype)
+        if g_qlast is not None:
+            gseed[0] = g_qlast
+    extra = None
+    if geo:
+        gQ, gn2, gq2, gp2 = _geometry_vjp(ctx, n, q, p, slope, x_save, g_tw if nz(g_tw) else None,
+                                          g_ss if nz(g_ss) else None)
+        gseed[1] = gQ
+        extra = (gn2, gq2, gp2)
     if g_runoff is None:
-        if ctx.gauge:
-            raise NotImplementedError("gauge-mode backward needs a runoff gradient")
-        g_runoff = torch.zeros((qprime.shape[1], T), device=qprime.device, dtype=qprime.dtype)
-    if g_qlast is not None:
-        if ctx.gauge:
-            if bool(g_qlast.ne(0).any()):
-                raise NotImplementedError("gradient through the final discharge state in gauge mode")
-        else:
-            # runoff[:, T-1] is the final state Q_{T-1}
-            g_runoff = g_runoff.clone()
-            g_runoff[:, T - 1] += g_qlast
+        G = g_off.numel() - 1 if ctx.gauge else N
+        g_runoff = torch.zeros((G, ctx.daily[2] if ctx.daily else T), device=qprime.device, dtype=qprime.dtype)
     # dL/dq' and dL/dQ0 (the carried state) when the caller's graph asks for them: route_timestep is
     # differentiable w.r.t. both in the reference (mmc.py:487-559), the hot start w.r.t. q'[0]
     want_qp = bool(ctx.needs_input_grad[0])
     want_q0 = bool(ctx.needs_input_grad[8])
     gn, gq, gp, gqp, gq0 = mc_route_backward(g_runoff, qprime, n, q, p, length, slope, x_storage, flow_scale, x_save,
-                                             bnd, g_off, g_idx, r_off, r_g, qp_valid, ctx.graph_id, ctx.consts,
+                                             bnd, g_off, g_idx, r_off, r_g, qp_valid, gseed, ctx.graph_id, ctx.consts,
                                              ctx.flags, T, ctx.qp_hours, ctx.daily, want_qp, want_q0)
     if ctx.p_scalar:
         gp = gp.sum().reshape(ctx.p_shape)
+    if extra is not None:
+        gn = gn + extra[0]
+        gq = gq + extra[1]
+        gp = gp + extra[2].reshape(gp.shape)
     return ((gqp if want_qp else None), gn, gq, gp) + (None,) * 4 + ((gq0 if want_q0 else None),) + (None,) * 11
 
 

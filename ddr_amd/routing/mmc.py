@@ -132,6 +132,8 @@ class MuskingumCunge:
         self.math = (getattr(cfg.params, "routing_math", None) or os.environ.get("DDR_ROUTING_MATH") or "faithful")
         if self.math not in ("exact", "faithful", "fast"):
             raise ValueError(f"routing_math must be 'exact', 'faithful' or 'fast', not {self.math!r}")
+        self._eager_nan_check = bool(getattr(cfg.params, "eager_nan_check", False)) or \
+            os.environ.get("DDR_EAGER_NAN_CHECK") == "1"
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None
@@ -227,7 +229,12 @@ class MuskingumCunge:
         assert self.q_prime is not None, "q_prime must be set before initializing discharge state"
         if self._graph is not None:
             # forward's launch runs the hot start as its step 0 and the NaN assertion of mmc.py:335 inside
-            # its q' gather (no separate pass over q'); reading _discharge_t first runs both here
+            # its q' gather (no separate pass over q'); reading _discharge_t first runs both here.  So a NaN
+            # q' raises at forward() (or at that first read), not here as in the reference -- unless the
+            # eager check is asked for (cfg.params.eager_nan_check or DDR_EAGER_NAN_CHECK=1: one host-synced
+            # reduction over q' per cold start, the reference's timing of the AssertionError)
+            if self._eager_nan_check:
+                _assert_no_nan(self.q_prime)
             self._state = None
             self._hot_pending = self.q_prime
         else:

@@ -303,6 +303,36 @@ ddr_status ddr_mc_backward_state_f64(const ddr_graph* g, const ddr_mc_consts* c,
                                      double* grad_p, double* grad_qprime, double* grad_q0, void* work,
                                      int32_t flags, void* stream);
 
+/* The general adjoint: ddr_mc_backward_state (grad_qprime, grad_q0 and work may be NULL: with both NULL
+ * this is ddr_mc_backward) plus per-reach gradients into the discharge state itself:
+ *   state_seed  (2, N) reference order, or NULL: row 0 dL/dQ_{T-1} -- the final state `_discharge_t`
+ *               (mmc.py:441, retained by dmc, torch_mc.py:196-216; an ordinary autograd tensor in gauge
+ *               mode too, mmc.py:433-441) -- and row 1 dL/dQ_{T-2}, the state the reported top width /
+ *               side slope of the last step were computed from (mmc.py:161-162; the caller forms it by
+ *               differentiating that geometry, e.g. from ddr_state_f32's Q_{T-2})
+ * Replaces: torch autograd through `_discharge_t` and `top_width` / `side_slope` after a forward. */
+ddr_status ddr_mc_backward_ex_f32(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                  const float* qprime, int64_t qprime_rows, int64_t T, const float* x_save,
+                                  const double* bnd, const float* grad_runoff, const ddr_gauges* gauges,
+                                  const float* state_seed, double* bwd_bnd, void* status, float* grad_n,
+                                  float* grad_q, float* grad_p, float* grad_qprime, float* grad_q0, void* work,
+                                  int32_t flags, void* stream);
+ddr_status ddr_mc_backward_ex_f64(const ddr_graph* g, const ddr_mc_consts* c, const ddr_mc_reaches* r,
+                                  const double* qprime, int64_t qprime_rows, int64_t T, const double* x_save,
+                                  const double* bnd, const double* grad_runoff, const ddr_gauges* gauges,
+                                  const double* state_seed, double* bwd_bnd, void* status, double* grad_n,
+                                  double* grad_q, double* grad_p, double* grad_qprime, double* grad_q0,
+                                  void* work, int32_t flags, void* stream);
+
+/* Q_t (N, reference order) from a forward's saved states: max(x(t), discharge_lb), or x(0) unclamped for a
+ * carried state (flags & DDR_FWD_CARRY) -- the routed discharge the reference holds as `_discharge_t`
+ * after step t (mmc.py:441, 557).  Enqueued on `stream`; 0 <= t < T.
+ * Replaces: reading MuskingumCunge._discharge_t / output[:, t] mid-window (mmc.py:428-441). */
+ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
+                         int32_t flags, float* out, void* stream);
+ddr_status ddr_state_f64(const ddr_graph* g, const double* x_save, int64_t T, int64_t t, double discharge_lb,
+                         int32_t flags, double* out, void* stream);
+
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,

@@ -523,8 +523,44 @@ def _celerity_vjp(Q, n, q, p, slope, bd: Bounds, g_c):
     return g_Q, g_n, g_qe, g_p
 
 
+def geometry_vjp(Q, n, q, p, slope, bd: Bounds, g_tw, g_ss):
+    """VJP of the reported geometry (trapezoidal.py:62-79 -> mmc.py:161-162: top_width = p depth^qe,
+    side_slope = clamp(top_width qe / (2 depth), 0.5, 50)) w.r.t. (Q, n, q_spatial, p_spatial), fp64; torch's
+    clamp backward is inclusive at both bounds.  g_tw / g_ss may be None."""
+    f = np.float64
+    Q, n, q, p, S = (np.asarray(a, f) for a in (Q, n, q, p, slope))
+    p = np.broadcast_to(p, Q.shape)
+    g_tw = np.zeros_like(Q) if g_tw is None else np.asarray(g_tw, f)
+    g_ss = np.zeros_like(Q) if g_ss is None else np.asarray(g_ss, f)
+    qe = q + 1e-6
+    num = Q * n * (qe + 1.0)
+    den = p * np.sqrt(S) + 1e-8
+    base = num / den
+    e = 3.0 / (5.0 + 3.0 * qe)
+    d0 = base ** e
+    depth = np.maximum(d0, bd.depth)
+    tw = p * depth ** qe
+    ss_raw = tw * qe / (2.0 * depth)
+    m_ss = (ss_raw >= 0.5) & (ss_raw <= 50.0)
+    gs = g_ss * m_ss
+    g_twt = g_tw + gs * qe / (2.0 * depth)
+    g_depth = g_twt * p * qe * depth ** (qe - 1.0) - gs * tw * qe / (2.0 * depth * depth)
+    g_p = g_twt * depth ** qe
+    g_qe = g_twt * tw * np.log(depth) + gs * tw / (2.0 * depth)
+    g_d0 = g_depth * (d0 >= bd.depth)
+    g_base = g_d0 * e * d0 / base
+    g_qe = g_qe + g_d0 * d0 * np.log(base) * (-9.0 / (5.0 + 3.0 * qe) ** 2)
+    g_num = g_base / den
+    g_p = g_p - g_base * num / (den * den) * np.sqrt(S)
+    g_Q = g_num * n * (qe + 1.0)
+    g_n = g_num * Q * (qe + 1.0)
+    g_qe = g_qe + g_num * Q * n
+    return g_Q, g_n, g_qe, g_p
+
+
 def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray, grad_runoff: np.ndarray,
-                   bd: Bounds = Bounds(), dt=3600.0, outflow_idx=None, want_qprime=False, carry=False):
+                   bd: Bounds = Bounds(), dt=3600.0, outflow_idx=None, want_qprime=False, carry=False,
+                   state_seed=None):
     """Adjoint of ``route`` w.r.t. (n, q_spatial, p_spatial) (and optionally q' and the state), fp64.
 
     ``xs`` is the (T, N) unclamped solve output of the forward (``xs[0]`` = Q0).
@@ -533,6 +569,8 @@ def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray,
     with ``want_qprime`` step 0 adds the hot start's transposed solve (mmc.py:25-66) to dL/dq'[0].
     ``carry``: the forward carried Q0 = ``xs[0]`` (``route(q0=...)``), which step 1 uses unclamped
     (mmc.py:330-342, 487-559); ``q0`` of the result is then dL/dQ0.
+    ``state_seed`` (2, N): per-reach dL/dQ_{T-1} (the final ``_discharge_t``, mmc.py:441) and dL/dQ_{T-2} (the
+    state of the reported geometry, mmc.py:161-162; ``geometry_vjp``), added to those steps' dL/dQ.
     """
     f = np.float64
     r = r.astype(f)
@@ -554,7 +592,12 @@ def route_backward(net: Network, r: Reaches, qprime: np.ndarray, xs: np.ndarray,
                 g_all[:, j] += G[g]
                 g_all[0, j] += G[g, 0] * (m0 - 1.0)
     else:
-        g_all = G.T
+        g_all = G.T.copy()
+    if state_seed is not None:
+        sd = np.asarray(state_seed, dtype=f)
+        g_all[T - 1] += sd[0]
+        if T >= 2:
+            g_all[T - 2] += sd[1]
     lam = np.zeros(N)
     gn = np.zeros(N)
     gq = np.zeros(N)

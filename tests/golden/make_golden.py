@@ -25,6 +25,9 @@ Fixtures:
                     _discharge_t, mmc.py:487-559; the hot start w.r.t. q'[0], mmc.py:25-66): dL/dstreamflow
                     of a hot-started forward, dL/dstreamflow + dL/dQ0 of a gauge-mode carried batch (one
                     gauge's carried sum below q_lb), and a 3-step route_timestep chain
+  chain.npz     F12 gradients out of the final state and the reported geometry: two chained gauge-mode
+                    batches (the second carries the first's _discharge_t with its graph), and one batch
+                    with the loss also on _discharge_t, top_width and side_slope (gauge / all-output mode)
   daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
                     downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
                     warmup 3, and torch autograd's d loss / d runoff
@@ -454,11 +457,69 @@ def make_state():
     np.savez_compressed(HERE / "state.npz", **out)
 
 
+def make_chain():
+    """F12: gradients out of the final discharge state and the reported geometry (the reference's autograd):
+    (a) two chained gauge-mode batches -- the second carries the first one's ``_discharge_t`` with its graph
+    (mmc.py:330-333, 433-441) and the loss is on both; (b) gauge mode and (c) all-output mode, one batch, the
+    loss also on ``_discharge_t``, ``top_width`` and ``side_slope`` (mmc.py:161-162, 441)."""
+    _, mmc = load_reference()
+    net = synthetic.random_binary_tree(90, seed=31)
+    T = 24
+    attrs = synthetic.reach_attributes(net.n, 31)
+    u = synthetic.unit_parameters(net.n, 31)
+    rng = np.random.default_rng(3100)
+    outflow = [np.array([-1]), np.array([10, 20, 31]), np.array([44]), np.array([5, 59, 60])]
+    flat = np.concatenate(outflow)
+    offs = np.cumsum([0] + [len(o) for o in outflow])
+    out = dict(n=np.int64(net.n), rows=net.rows, cols=net.cols, length=attrs.length, slope=attrs.slope, x=attrs.x,
+               outflow_flat=flat, outflow_offsets=offs, **{f"u_{k}": v for k, v in u.items()})
+    leaf = lambda: {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in u.items()}  # noqa: E731
+    grads = lambda sp_: {f"grad_{k}": v.grad.numpy().copy() for k, v in sp_.items()}  # noqa: E731
+
+    # (a) two chained gauge-mode batches, one engine, the carried state keeps its graph
+    q1 = synthetic.lateral_inflow(net.n, T, 31)
+    q2 = synthetic.lateral_inflow(net.n, T, 31, t0=T)
+    W1 = rng.uniform(0, 1, (len(outflow), T)).astype(np.float32)
+    W2 = rng.uniform(0, 1, (len(outflow), T)).astype(np.float32)
+    dc = routing_dc(net.n, net.rows, net.cols, attrs, outflow)
+    mc = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+    spa = leaf()
+    mc.setup_inputs(dc, torch.from_numpy(q1), spa)
+    o1 = mc.forward()
+    mc.setup_inputs(dc, torch.from_numpy(q2), spa, carry_state=True)
+    o2 = mc.forward()
+    ((o1 * torch.from_numpy(W1)).sum() + (o2 * torch.from_numpy(W2)).sum()).backward()
+    out.update(qprime_a1=q1, qprime_a2=q2, W_a1=W1, W_a2=W2, ref_a_out1=o1.detach().numpy(),
+               ref_a_out2=o2.detach().numpy(), **{f"ref_a_{k}": v for k, v in grads(spa).items()})
+
+    # (b) gauge mode / (c) all-output mode: loss on the output, _discharge_t, top_width and side_slope
+    for tag, ofx in (("b", outflow), ("c", None)):
+        qb = synthetic.lateral_inflow(net.n, T, 32 if tag == "b" else 33)
+        G = len(ofx) if ofx is not None else net.n
+        Wb = rng.uniform(0, 1, (G, T)).astype(np.float32)
+        V = rng.uniform(-1, 1, (3, net.n)).astype(np.float32)
+        dcb = routing_dc(net.n, net.rows, net.cols, attrs, ofx)
+        mcb = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+        spb = leaf()
+        mcb.setup_inputs(dcb, torch.from_numpy(qb), spb)
+        ob = mcb.forward()
+        Vt = torch.from_numpy(V)
+        loss = ((ob * torch.from_numpy(Wb)).sum() + (mcb._discharge_t * Vt[0]).sum() + (mcb.top_width * Vt[1]).sum()
+                + (mcb.side_slope * Vt[2]).sum())
+        loss.backward()
+        out.update({f"qprime_{tag}": qb, f"W_{tag}": Wb, f"V_{tag}": V, f"ref_{tag}_out": ob.detach().numpy(),
+                    f"ref_{tag}_q_last": mcb._discharge_t.detach().numpy(),
+                    f"ref_{tag}_top_width": mcb.top_width.detach().numpy(),
+                    f"ref_{tag}_side_slope": mcb.side_slope.detach().numpy(),
+                    **{f"ref_{tag}_{k}": v for k, v in grads(spb).items()}})
+    np.savez_compressed(HERE / "chain.npz", **out)
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
             {"geostats": make_geostats, "daily": make_daily, "collate": make_collate, "deep": make_deep,
-             "state": make_state}[name]()
+             "state": make_state, "chain": make_chain}[name]()
         return
     torch.manual_seed(0)
     utils, mmc = load_reference()
@@ -511,6 +572,7 @@ def main():
     make_geostats()
     make_daily()
     make_state()
+    make_chain()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

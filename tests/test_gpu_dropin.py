@@ -294,3 +294,31 @@ def test_nan_streamflow_asserts_like_the_reference(cuda):
     mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
     mc.setup_inputs(golden_dataclass(case), q, sp_params)  # no assertion
     mc.forward()
+    # the opt-in eager check raises inside setup_inputs, as the reference does (mmc.py:335)
+    q = torch.from_numpy(case.qprime).clone()
+    q[4, 9] = float("nan")
+    cfg = cfg_of(PARAMS_DEFAULT)
+    cfg.params.eager_nan_check = True
+    mc = MuskingumCunge(cfg, device=cuda)
+    with pytest.raises(AssertionError, match="NaN flows"):
+        mc.setup_inputs(golden_dataclass(case), q, sp_params)
+
+
+def test_nan_check_on_a_side_stream(cuda):
+    """The cold-start NaN verdict is recorded per device on the launch's own stream (capi.cpp NanCheck):
+    checked forwards on a non-default stream, one after another, each see only their own q'."""
+    case, _ = golden_case("tree300", PARAMS_DEFAULT)
+    sp_params = {k: torch.from_numpy(v).to(cuda) for k, v in case.u.items()}
+    s = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s):
+        model = dmc(cfg_of(PARAMS_DEFAULT), device=cuda)
+        out = model(routing_dataclass=golden_dataclass(case), streamflow=torch.from_numpy(case.qprime),
+                    spatial_parameters=sp_params)["runoff"]
+        q = torch.from_numpy(case.qprime).clone()
+        q[3, 2] = float("nan")
+        with pytest.raises(AssertionError, match="NaN flows"):
+            model(routing_dataclass=golden_dataclass(case), streamflow=q, spatial_parameters=sp_params)
+        out2 = model(routing_dataclass=golden_dataclass(case), streamflow=torch.from_numpy(case.qprime),
+                     spatial_parameters=sp_params)["runoff"]
+    s.synchronize()
+    assert torch.equal(out, out2)

@@ -195,3 +195,120 @@ def test_state_gradient_off_by_default_and_partition_invariant(cuda):
         assert np.array_equal(outs[0][0][k], outs[1][0][k]), k
         assert np.array_equal(outs[1][0][k], outs[2][0][k]), k
     assert np.array_equal(outs[1][1], outs[2][1])
+
+
+def _dropin(case, outflow, cuda):
+    """A drop-in MuskingumCunge on the case's network (RoutingDataclass stand-in: CSR adjacency)."""
+    from types import SimpleNamespace
+
+    import scipy.sparse as sp
+
+    from ddr_amd.routing.mmc import MuskingumCunge
+
+    a = sp.coo_matrix((np.ones(len(case.rows), np.float32), (case.rows, case.cols)), shape=(case.n, case.n)).tocsr()
+    adj = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)), torch.from_numpy(a.indices.astype(np.int64)),
+                                  torch.from_numpy(a.data), size=(case.n, case.n))
+    dc = SimpleNamespace(adjacency_matrix=adj, length=torch.from_numpy(case.length), slope=torch.from_numpy(case.slope),
+                         x=torch.from_numpy(case.x), top_width=torch.empty(0), side_slope=torch.empty(0),
+                         outflow_idx=outflow, gage_catchment=None, observations=None, flow_scale=None)
+    cfg = SimpleNamespace(params=SimpleNamespace(**PARAMS_DEFAULT))
+    return MuskingumCunge(cfg, device=cuda), dc
+
+
+def test_chained_gauge_batches_backpropagate_into_the_first_state(cuda):
+    """F12 (a): the second gauge-mode batch carries the first one's _discharge_t with its graph
+    (mmc.py:330-333, 433-441); one loss over both batches reaches the first batch through its final state
+    (the adjoint's q_last seed in gauge mode), as the reference's autograd does."""
+    from test_oracle import _chain_case
+
+    case, d, outflow = _chain_case()
+    mc, dc = _dropin(case, outflow, cuda)
+    sp_params = {k: torch.from_numpy(v).to(cuda).requires_grad_(True) for k, v in case.u.items()}
+    mc.setup_inputs(dc, torch.from_numpy(d["qprime_a1"]).to(cuda), sp_params)
+    o1 = mc.forward()
+    mc.setup_inputs(dc, torch.from_numpy(d["qprime_a2"]).to(cuda), sp_params, carry_state=True)
+    o2 = mc.forward()
+    ((o1 * torch.from_numpy(d["W_a1"]).to(cuda)).sum() + (o2 * torch.from_numpy(d["W_a2"]).to(cuda)).sum()).backward()
+    assert maxrel(o1.detach().cpu().numpy(), d["ref_a_out1"]) <= 1e-4
+    assert maxrel(o2.detach().cpu().numpy(), d["ref_a_out2"]) <= 1e-4
+    for k in ("n", "q_spatial", "p_spatial"):
+        assert normrel(sp_params[k].grad.cpu().numpy(), d[f"ref_a_grad_{k}"]) <= 5e-5, k
+
+
+@pytest.mark.parametrize("tag", ["b", "c"], ids=["gauge", "all_output"])
+def test_final_state_and_geometry_gradients_match_reference(cuda, tag):
+    """F12 (b, c): a loss on the output, on _discharge_t (retained by dmc, torch_mc.py:196-216) and on the
+    reported top_width / side_slope (mmc.py:161-162) -- gauge and all-output mode."""
+    from test_oracle import _chain_case
+
+    case, d, outflow = _chain_case()
+    mc, dc = _dropin(case, outflow if tag == "b" else None, cuda)
+    sp_params = {k: torch.from_numpy(v).to(cuda).requires_grad_(True) for k, v in case.u.items()}
+    mc.setup_inputs(dc, torch.from_numpy(d[f"qprime_{tag}"]).to(cuda), sp_params)
+    out = mc.forward()
+    V = torch.from_numpy(d[f"V_{tag}"]).to(cuda)
+    loss = ((out * torch.from_numpy(d[f"W_{tag}"]).to(cuda)).sum() + (mc._discharge_t * V[0]).sum()
+            + (mc.top_width * V[1]).sum() + (mc.side_slope * V[2]).sum())
+    loss.backward()
+    assert maxrel(out.detach().cpu().numpy(), d[f"ref_{tag}_out"]) <= 1e-4
+    assert maxrel(mc.top_width.detach().cpu().numpy(), d[f"ref_{tag}_top_width"]) <= 1e-4
+    for k in ("n", "q_spatial", "p_spatial"):
+        assert normrel(sp_params[k].grad.cpu().numpy(), d[f"ref_{tag}_grad_{k}"]) <= 5e-5, (tag, k)
+
+
+@pytest.mark.parametrize("gkw", PARTITIONS, ids=["whole", "cut"])
+@pytest.mark.parametrize("gauge", [False, True], ids=["all_output", "gauge"])
+def test_fp64_seeded_adjoint_matches_fp64_oracle(cuda, gkw, gauge):
+    """fp64 kernel vs the fp64 oracle with the state seeds (dL/d q_last) and the geometry VJP, plus dL/dq'
+    (the state-gradient kernel reads the seeds too)."""
+    from test_oracle import _chain_case, oracle_seeded_grads
+
+    case, d, outflow = _chain_case()
+    ofx = outflow if gauge else None
+    u, n, q, p, slope, tt = physical(case, cuda, torch.float64)
+    T = 24
+    qp = tt(d["qprime_b"]).requires_grad_(True)
+    g = RiverGraph(case.n, case.rows, case.cols, **(gkw or {}))
+    gz = GaugeMap.build(ofx, case.n, cuda) if gauge else None
+    runoff, q_last, tw, ss = route(g, qp, n, q, p, tt(case.length), slope, tt(case.x), gauges=gz, consts=C)
+    rng = np.random.default_rng(5)
+    W = rng.uniform(0, 1, tuple(runoff.shape))
+    V = rng.uniform(-1, 1, (3, case.n))
+    loss = (runoff * tt(W)).sum() + (q_last * tt(V[0])).sum() + (tw * tt(V[1])).sum() + (ss * tt(V[2])).sum()
+    loss.backward()
+    net, r, bd = case.network(), reaches_of(n, q, p, slope, case, np.float64), case.bounds
+    res, gpar = oracle_seeded_grads(case, net, r, bd, d["qprime_b"].astype(np.float64), W, ofx, V, T)
+    assert maxrel(runoff.detach().cpu().numpy(), res["runoff"]) <= 1e-12
+    for k, v in gpar.items():
+        assert normrel(u[k].grad.cpu().numpy(), v) <= 1e-10, k
+    assert qp.grad is not None and bool(torch.isfinite(qp.grad).all())
+
+
+def test_fp64_backward_single_buffer_at_kr2(cuda):
+    """fp64 at two reaches per thread: the double-buffered backward slots (96 B per slot) do not fit the LDS
+    for blocks above ~1.67K reaches, so the launch takes the single-buffered variant (bwd_xb_of) instead of failing
+    with DDR_ERR_CAPACITY; gradients equal the fp64 oracle's."""
+    net = synthetic.random_binary_tree(1900, seed=41)
+    T = 24
+    at = synthetic.reach_attributes(net.n, 41)
+    from conftest import Case
+
+    case = Case(net.n, net.rows, net.cols, at.length, at.slope, at.x, None, None,
+                synthetic.unit_parameters(net.n, 41), PARAMS_DEFAULT)
+    u, n, q, p, slope, tt = physical(case, cuda, torch.float64)
+    g = RiverGraph(net.n, net.rows, net.cols, target_blocks=1)  # one 1900-reach block
+    assert g.info.reaches_per_thread == 2 and g.info.n_blocks == 1
+    qs = synthetic.lateral_inflow(net.n, T, 41).astype(np.float64)
+    runoff, _, _, _ = route(g, tt(qs), n, q, p, tt(at.length), slope, tt(at.x), consts=C)
+    W = np.random.default_rng(41).uniform(0, 1, tuple(runoff.shape))
+    runoff.backward(tt(W))
+    r = reaches_of(n, q, p, slope, case, np.float64)
+    netO = O.Network.from_coo(net.n, net.rows, net.cols)
+    res = O.route(netO, r, qs, case.bounds, dtype=np.float64)
+    assert maxrel(runoff.detach().cpu().numpy(), res["runoff"]) <= 1e-12
+    bw = O.route_backward(netO, r, qs, res["x"], W, case.bounds)
+    gpar = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], case.u["n"].astype(np.float64),
+                                   case.u["q_spatial"].astype(np.float64), case.u["p_spatial"].astype(np.float64),
+                                   case.params["parameter_ranges"])
+    for k, v in gpar.items():
+        assert normrel(u[k].grad.cpu().numpy(), v) <= 1e-10, k

@@ -208,3 +208,57 @@ def test_oracle_state_gradients_match_reference():
                                 case.u["p_spatial"], case.params["parameter_ranges"])
     for k, v in g.items():
         assert normrel(v, d[f"ref_c_grad_{k}"]) < GRAD_TOL, k
+
+
+def _chain_case():
+    from conftest import Case
+
+    d = load_golden("chain")
+    u = {k: d[f"u_{k}"] for k in ("n", "q_spatial", "p_spatial")}
+    case = Case(int(d["n"]), d["rows"], d["cols"], d["length"], d["slope"], d["x"], d["qprime_a1"], d["W_a1"], u,
+                PARAMS_DEFAULT)
+    offs = d["outflow_offsets"]
+    outflow = [d["outflow_flat"][offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+    return case, d, outflow
+
+
+def oracle_seeded_grads(case, net, r, bd, qprime, W, outflow, V, T):
+    """Forward + adjoint with the loss also on _discharge_t (V[0]), top_width (V[1]) and side_slope (V[2]):
+    the geometry's VJP at Q_{T-2} seeds the adjoint's state at T - 2 and adds its own parameter terms."""
+    res = O.route(net, r, qprime, bd, dtype=np.float64, outflow_idx=outflow)
+    Qp = np.maximum(res["x"][T - 2], bd.discharge)
+    gQ, gn2, gq2, gp2 = O.geometry_vjp(Qp, r.n, r.q, r.p, r.slope, bd, V[1], V[2])
+    bw = O.route_backward(net, r, qprime, res["x"], W, bd, outflow_idx=outflow, state_seed=np.stack([V[0], gQ]))
+    g = O.param_grads_from_unit(bw["n"] + gn2, bw["q_spatial"] + gq2, bw["p_spatial"] + gp2, case.u["n"],
+                                case.u["q_spatial"], case.u["p_spatial"], case.params["parameter_ranges"])
+    return res, g
+
+
+def test_oracle_chain_and_geometry_gradients_match_reference():
+    """F12: (a) two chained gauge-mode batches, the second carrying the first one's state with its graph --
+    dL/dQ0 of batch 2 seeds batch 1's final state; (b, c) a loss also on _discharge_t, top_width and
+    side_slope (gauge and all-output mode): the state seeds + the geometry VJP against the reference's
+    autograd."""
+    case, d, outflow = _chain_case()
+    net, r, bd = case.network(), case.reaches(), case.bounds
+    T = d["qprime_a1"].shape[0]
+    # (a)
+    r1 = O.route(net, r, d["qprime_a1"], bd, dtype=np.float64, outflow_idx=outflow)
+    r2 = O.route(net, r, d["qprime_a2"], bd, q0=r1["q_last"], dtype=np.float64, outflow_idx=outflow)
+    assert maxrel(r1["runoff"], d["ref_a_out1"]) < FWD_TOL
+    assert maxrel(r2["runoff"], d["ref_a_out2"]) < FWD_TOL
+    b2 = O.route_backward(net, r, d["qprime_a2"], r2["x"], d["W_a2"], bd, outflow_idx=outflow, carry=True)
+    b1 = O.route_backward(net, r, d["qprime_a1"], r1["x"], d["W_a1"], bd, outflow_idx=outflow,
+                          state_seed=np.stack([b2["q0"], np.zeros(case.n)]))
+    assert np.abs(b2["q0"]).max() > 0
+    g = O.param_grads_from_unit(b1["n"] + b2["n"], b1["q_spatial"] + b2["q_spatial"], b1["p_spatial"] + b2["p_spatial"],
+                                case.u["n"], case.u["q_spatial"], case.u["p_spatial"], case.params["parameter_ranges"])
+    for k, v in g.items():
+        assert normrel(v, d[f"ref_a_grad_{k}"]) < GRAD_TOL, k
+    # (b) gauge mode, (c) all-output mode
+    for tag, ofx in (("b", outflow), ("c", None)):
+        res, g = oracle_seeded_grads(case, net, r, bd, d[f"qprime_{tag}"], d[f"W_{tag}"], ofx, d[f"V_{tag}"], T)
+        assert maxrel(res["runoff"], d[f"ref_{tag}_out"]) < FWD_TOL
+        assert maxrel(res["top_width"], d[f"ref_{tag}_top_width"]) < FWD_TOL
+        for k, v in g.items():
+            assert normrel(v, d[f"ref_{tag}_grad_{k}"]) < GRAD_TOL, (tag, k)
