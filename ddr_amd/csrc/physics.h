@@ -25,6 +25,7 @@ struct Consts {
   R dt, qlb, vlb, vub, dlb, bwlb, sslb, ssub;
   PowK pk;        // fp64 constants of the fp32 pow (register-pinned by the routing kernels)
   double ln_dlb;  // ln of the depth lower bound (fp64, host-computed)
+  float pinf = __builtin_inff();  // +inf of the one-med3 clamps (rmaxc; an opaque copy at KR = 4)
 };
 
 __device__ __forceinline__ float dv(float a, float b) { return div_rn(a, b); }
@@ -91,6 +92,19 @@ __device__ __forceinline__ R rclamp(R x, R lo, R hi) { return rmin(rmax(x, lo), 
 // fp32: one v_med3_f32 each (equal to torch.clamp for the finite values of the physics)
 __device__ __forceinline__ float rmax(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, __builtin_inff()); }
 __device__ __forceinline__ float rmin(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, -__builtin_inff()); }
+// The same with the kernel's infinity (Consts::pinf): with a literal infinity the compiler turns med3(a, b, inf)
+// into max(a, b) and, in IEEE mode, canonicalises both operands first (two extra v_max_f32 per clamp); the
+// heavy-load kernels (KR = 4) hand it an infinity it cannot see through (opaque_inf, one VGPR), which keeps
+// the single med3 -- C5 forward -1.5 %, C3 backward -3 %; at light load the extra VGPR costs more than the
+// instructions save, so those kernels keep the literal (profiles/r05/ab_r05.txt)
+__device__ __forceinline__ float opaque_inf(float v) {
+  asm("" : "+v"(v));  // not volatile: hoisted out of loops like any pure value
+  return v;
+}
+template <typename C>
+__device__ __forceinline__ float rmaxc(float a, float b, const C& c) { return __builtin_amdgcn_fmed3f(a, b, c.pinf); }
+template <typename C>
+__device__ __forceinline__ double rmaxc(double a, double b, const C&) { return rmax(a, b); }
 __device__ __forceinline__ float rclamp(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 
 // torch.clamp(min=) with its NaN propagation (v_med3_f32 would return the bound for a NaN): used for
@@ -157,13 +171,13 @@ __device__ __forceinline__ void coefficients(const ReachStatic<R>& s, R Q, const
   const R num = (Q * s.n) * s.qe1();
   const R ratio = dvf<Fast>(num, s.dd);
   const R pwv = pwf<Fast>(ratio, s.expo, gk ? &ln_ratio : nullptr, c.pk);
-  const R depth = rmax(pwv, c.dlb);
+  const R depth = rmaxc(pwv, c.dlb, c);
   const R dq = pwf<Fast>(depth, s.qe, gk ? &ln_depth : nullptr, c.pk);
   const R tw = s.p * dq;
   const R ssr = dvf<Fast>(tw * s.qe, R(2) * depth);
   const R ss = rclamp(ssr, c.sslb, c.ssub);
   const R bwr = tw - (R(2) * ss) * depth;
-  const R bw = rmax(bwr, c.bwlb);
+  const R bw = rmaxc(bwr, c.bwlb, c);
   const R area = ((tw + bw) * depth) * R(0.5);  // x / 2 == x * 0.5 exactly
   const R sq = sqf1p<Fast>(R(1) + ss * ss);
   const R wp = bw + (R(2) * depth) * sq;
@@ -229,7 +243,7 @@ __device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], c
     exp_np<NP>(z, E, c.pk);
     DDR_FOR_NP {
       const float pw = (float)E[h];
-      depth[h] = rmax(pw, c.dlb);
+      depth[h] = rmaxc(pw, c.dlb, c);
       const double u = ((double)pw - E[h]) * __builtin_amdgcn_rcp(E[h]);
       l[h] = (pw >= c.dlb) ? z[h] + fma(-0.5 * u, u, u) : c.ln_dlb;
       z[h] = (double)s[h].qe * l[h];
@@ -239,7 +253,7 @@ __device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], c
   } else {
     DDR_FOR_NP e[h] = s[h].expo;
     pw_np<NP>(ratio, e, depth, c.pk);
-    DDR_FOR_NP depth[h] = rmax(depth[h], c.dlb);
+    DDR_FOR_NP depth[h] = rmaxc(depth[h], c.dlb, c);
     DDR_FOR_NP e[h] = s[h].qe;
     pw_np<NP>(depth, e, dq, c.pk);
   }
@@ -249,7 +263,7 @@ __device__ __forceinline__ void coefficients_np(const ReachStatic<R> (&s)[NP], c
   dv_np<NP>(a, b, ssr);
   DDR_FOR_NP ss[h] = rclamp(ssr[h], c.sslb, c.ssub);
   DDR_FOR_NP o[h].ss = ss[h];
-  DDR_FOR_NP bw[h] = rmax(o[h].tw - (R(2) * ss[h]) * depth[h], c.bwlb);
+  DDR_FOR_NP bw[h] = rmaxc(o[h].tw - (R(2) * ss[h]) * depth[h], c.bwlb, c);
   DDR_FOR_NP area[h] = ((o[h].tw + bw[h]) * depth[h]) * R(0.5);
   DDR_FOR_NP a[h] = sq1p(R(1) + ss[h] * ss[h]);
   DDR_FOR_NP wp[h] = bw[h] + (R(2) * depth[h]) * a[h];
@@ -283,14 +297,14 @@ __device__ __forceinline__ PhysOut<float> coefficients_fast(const ReachStatic<fl
   const float qe = s.qe;
   const float ratio = ((Q * s.n) * (qe + 1.0f)) * __builtin_amdgcn_rcpf(s.dd);
   const float pw = __builtin_amdgcn_exp2f(s.expo * __builtin_amdgcn_logf(ratio));
-  const float depth = rmax(pw, c.dlb);
+  const float depth = rmaxc(pw, c.dlb, c);
   const float dq = __builtin_amdgcn_exp2f(qe * __builtin_amdgcn_logf(depth));
   PhysOut<float> o;
   o.tw = s.p * dq;
   const float td = depth + depth;
   const float ssr = (o.tw * qe) * __builtin_amdgcn_rcpf(td);
   o.ss = rclamp(ssr, c.sslb, c.ssub);
-  const float bw = rmax(o.tw - (o.ss + o.ss) * depth, c.bwlb);
+  const float bw = rmaxc(o.tw - (o.ss + o.ss) * depth, c.bwlb, c);
   const float area = ((o.tw + bw) * depth) * 0.5f;
   const float u = fmaf(o.ss, o.ss, 1.0f);
   const float wp = fmaf(td, u * __builtin_amdgcn_rsqf(u), bw);
@@ -314,12 +328,12 @@ __device__ __forceinline__ PhysOut<float> coefficients_faithful(const ReachStati
                                                                 const Consts<float>& c) {
   PhysOut<float> o;
   const float ratio = div_rn((Q * s.n) * s.qe1(), s.dd);
-  const float depth = rmax(pow_faithful(ratio, s.expo), c.dlb);
+  const float depth = rmaxc(pow_faithful(ratio, s.expo), c.dlb, c);
   const float dq = pow_faithful(depth, s.qe);
   o.tw = s.p * dq;
   const float ssr = div_rn(o.tw * s.qe, 2.0f * depth);
   o.ss = rclamp(ssr, c.sslb, c.ssub);
-  const float bw = rmax(o.tw - (2.0f * o.ss) * depth, c.bwlb);
+  const float bw = rmaxc(o.tw - (2.0f * o.ss) * depth, c.bwlb, c);
   const float area = ((o.tw + bw) * depth) * 0.5f;
   const float wp = bw + (2.0f * depth) * sqrt_rn_normal(1.0f + o.ss * o.ss);
   const float Rh = div_rn(area, wp);
@@ -448,7 +462,7 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
   const float ratio = num * rdd;
   const float l2r = __builtin_amdgcn_logf(ratio);
   const float pw = __builtin_amdgcn_exp2f(expo * l2r);
-  const float depth = rmax(pw, c.dlb);
+  const float depth = rmaxc(pw, c.dlb, c);
   const float l2d = __builtin_amdgcn_logf(depth);
   const float dq = __builtin_amdgcn_exp2f(qe * l2d);
   const float tw = s.p * dq;
@@ -457,7 +471,7 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
   const float ssr = (tw * qe) * rtd;
   const float ss = rclamp(ssr, c.sslb, c.ssub);
   const float bwr = tw - (ss + ss) * depth;
-  const float bw = rmax(bwr, c.bwlb);
+  const float bw = rmaxc(bwr, c.bwlb, c);
   const float area = ((tw + bw) * depth) * 0.5f;
   const float u = fmaf(ss, ss, 1.0f);
   const float isq = __builtin_amdgcn_rsqf(u);

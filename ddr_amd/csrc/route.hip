@@ -253,18 +253,23 @@ constexpr unsigned kWaitVmcnt0 = 0x0F70;
 
 // Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
 // pin_pow: keep the fp64 constants of the correctly rounded pow in VGPRs (kernels that evaluate it).
+// opq_inf: the clamps' infinity opaque to the compiler (rmaxc: one v_med3_f32 per clamp; the KR = 4 kernels)
+#ifndef DDR_OPQ_INF_MIN_KR
+#define DDR_OPQ_INF_MIN_KR 4
+#endif
 template <typename R>
-__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a, bool pin_pow = true);
+__device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a, bool pin_pow = true, bool opq_inf = false);
 template <>
-__device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a, bool pin_pow) {
+__device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a, bool pin_pow, bool opq_inf) {
 #ifndef DDR_PIN_POWK
 #define DDR_PIN_POWK 1
 #endif
   return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7],
-                       (DDR_PIN_POWK && pin_pow) ? pow_consts_vgpr() : pow_consts(), a.ln_dlb};
+                       (DDR_PIN_POWK && pin_pow) ? pow_consts_vgpr() : pow_consts(), a.ln_dlb,
+                       opq_inf ? opaque_inf(__builtin_inff()) : __builtin_inff()};
 }
 template <>
-__device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a, bool) {
+__device__ __forceinline__ Consts<double> consts_of<double>(const RouteArgs& a, bool, bool) {
   return Consts<double>{a.c[0], a.c[1], a.c[2], a.c[3], a.c[4], a.c[5], a.c[6], a.c[7], pow_consts(), a.ln_dlb};
 }
 
@@ -304,8 +309,29 @@ __device__ __forceinline__ V opq(V x) {
 }
 __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
 // 16-B runoff row segments (plain stores: measured faster than 8-B segments and than nt stores)
+#ifndef DDR_RUNOFF_NT
+#define DDR_RUNOFF_NT 0
+#endif
 __device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
+  if (DDR_RUNOFF_NT) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = {a, b, c, d};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
+    return;
+  }
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+#ifndef DDR_GRAD_NT
+#define DDR_GRAD_NT 0
+#endif
+// a dL/drunoff group (streamed: each 16-B piece of a row is read once per launch)
+__device__ __forceinline__ float4 load_grad4(const float* p) {
+  if (DDR_GRAD_NT) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return *reinterpret_cast<const float4*>(p);
 }
 __device__ __forceinline__ void store4(double* p, double a, double b, double c, double d) {
   reinterpret_cast<double2*>(p)[0] = make_double2(a, b);
@@ -480,7 +506,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const StatTab<R> tab{reinterpret_cast<R*>(sx + kXBuf * S)};           // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 * kXBuf + 6 * sizeof(R))));  // [nvirt][kChunkFwd]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
-  const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith);
+  const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith, KR >= DDR_OPQ_INF_MIN_KR);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool accum = a.flags & DDR_FWD_ACCUMULATE;  // every step a hot start (daily accumulation)
@@ -797,7 +823,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const int t = tau - off_of(k);
         const int nup = up_n(up[k]);
         const R qv = qcur[k];  // q' * flow_scale (mmc.py:303-304), applied by the gather
-        const R qc = rmax(qv, cs.qlb);                                        // mmc.py:421-424
+        const R qc = rmaxc(qv, cs.qlb, cs);                                        // mmc.py:421-424
         const R b = ((ph[h].c2 * In[k]) + (ph[h].c3 * Q[k])) + (ph[h].c4 * qc);  // mmc.py:535-538
         const double x0v = x0a[h];
         double x1v = x1a[h];
@@ -806,7 +832,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const bool raw = !kSt && (t == 0 && carry);
         auto qf = [&](double x) -> R {
           const R xr = R(x);
-          return raw ? xr : rmax(xr, cs.qlb);
+          return raw ? xr : rmaxc(xr, cs.qlb, cs);
         };
         const double dc1 = (double)ph[h].c1;
         double acc = (double)b;                                         // utils.py:587-600 (fp64)
@@ -849,7 +875,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             ob2[k] = ob3[k];
             ob3[k] = rmax_nan(xr, cs.qlb);
             R* orow = runoff + (int64_t)ref[k] * T;
-            if (!emit4) orow[t] = ob3[k];
+#ifndef DDR_EXP_RUNOFF_DUMMY
+#define DDR_EXP_RUNOFF_DUMMY 0  // timing experiment only: runoff stores into a 256-KB window (wrong results)
+#endif
+            if (DDR_EXP_RUNOFF_DUMMY) {
+              if ((t & 3) == 3) store4(runoff + ((int64_t)(ref[k] & 1023) << 6) + ((t - 3) & 60), ob0[k], ob1[k], ob2[k], ob3[k]);
+            } else if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
           if (B.ncout > 0 && (off[k] >> 16) && !(DDR_FWD_STORER_GRANULES && storer_mode)) {
@@ -1101,7 +1132,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const StatTab<R> tab{sx + kXB * S};                   // [S][6]
   R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * (3 * kXB + 6) * sizeof(R)));  // [ncout][kChunkBwd][2]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                                            // confluence lists
-  const Consts<R> cs = consts_of<R>(a);
+  const Consts<R> cs = consts_of<R>(a, true, KR >= DDR_OPQ_INF_MIN_KR);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool force_to = a.flags & kFlagForceTimeout;
@@ -1126,6 +1157,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
   // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
   R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  // the gradient groups as shift registers (KR <= 2: c3s8 backward -4 %); at KR = 4 the select on t & 3 measured
+  // faster (C5 backward 59.5 vs 57.3 ms, profiles/r05/ab_r05.txt)
+#ifndef DDR_BWD_SHIFT_MAX_KR
+#define DDR_BWD_SHIFT_MAX_KR 2
+#endif
+  constexpr bool kShiftG = KR <= DDR_BWD_SHIFT_MAX_KR;
   // early loads (DDR_BWD_EARLY_LOADS): the next tick's x(t - 3) and virtual x are requested at the top
   // of the tick into a second register set (roles swap every tick: the loop is unrolled by two), so
   // they have the whole tick to land instead of the part after the first barrier
@@ -1261,44 +1298,62 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     return a.bnd[(int64_t)v_edge * T + tc];
   };
   // dL/drunoff of steps base .. base + 3 of reach slice k (mmc.py:380-412: runoff[ref, t] = Q_t; in
-  // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439)
-  auto load_grad_out = [&](int ref, int64_t base, int gs) {
+  // gauge mode every gauge sums its reaches' Q_t, mmc.py:405-411, 433-439).  `base` is 4-aligned except
+  // for a reach's first group (un: base = T - 4, any alignment; steps outside [0, T) read clamped rows and
+  // are never consumed)
+  auto load_grad_out = [&](int ref, int64_t base, int gs, bool un) {
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
-    const int64_t i1 = base + 1 < T ? base + 1 : T - 1, i2 = base + 2 < T ? base + 2 : T - 1,
-                  i3 = base + 3 < T ? base + 3 : T - 1;
+    const bool v4 = vec4 && !(un && (base & 3) != 0);
+    auto cl = [&](int64_t i) { return i < 0 ? int64_t(0) : (i < T ? i : T - 1); };
+    const int64_t i0 = cl(base), i1 = cl(base + 1), i2 = cl(base + 2), i3 = cl(base + 3);
     // m0: the gauge's t = 0 sum passed its clamp (state gradients only; mmc.py:398-412)
     auto add_row = [&](const R* row, bool m0) {
-      if (vec4) {
+      if (v4) {
         if constexpr (sizeof(R) == 4) {
-          const float4 v = *reinterpret_cast<const float4*>(row + base);
-          v0 = v0 + (m0 ? v.x : 0.0f); v1 = v1 + v.y; v2 = v2 + v.z; v3 = v3 + v.w;
+          const float4 v = load_grad4(row + base);
+          v0 = v0 + ((m0 || base != 0) ? v.x : 0.0f); v1 = v1 + v.y; v2 = v2 + v.z; v3 = v3 + v.w;
         } else {
           const double2 u = reinterpret_cast<const double2*>(row + base)[0];
           const double2 w = reinterpret_cast<const double2*>(row + base)[1];
-          v0 = v0 + (m0 ? u.x : 0.0); v1 = v1 + u.y; v2 = v2 + w.x; v3 = v3 + w.y;
+          v0 = v0 + ((m0 || base != 0) ? u.x : 0.0); v1 = v1 + u.y; v2 = v2 + w.x; v3 = v3 + w.y;
         }
       } else {
-        v0 = v0 + (m0 ? row[base] : R(0)); v1 = v1 + row[i1]; v2 = v2 + row[i2]; v3 = v3 + row[i3];
+        v0 = v0 + ((m0 || base != 0) ? row[i0] : R(0));
+        v1 = v1 + ((m0 || base != -1) ? row[i1] : R(0));
+        v2 = v2 + ((m0 || base != -2) ? row[i2] : R(0));
+        v3 = v3 + ((m0 || base != -3) ? row[i3] : R(0));
       }
     };
     if (a.g_roff) {
+      const bool z = GS && a.gmask0 && base <= 0;  // the group holds step 0
       if (gs >= 0) {
         // the reach's only gauge (kGReg): the row address needs no dependent index loads in the tick
-        add_row(gout + (int64_t)gs * T, !(GS && base == 0 && a.gmask0 && a.gmask0[gs] == 0));
+        add_row(gout + (int64_t)gs * T, !(z && a.gmask0[gs] == 0));
         return make_grad4(v0, v1, v2, v3);
       }
       const int64_t q1 = a.g_roff[ref + 1];
       for (int64_t q = a.g_roff[ref]; q < q1; ++q) {
         const int64_t gi = a.g_rg[q];
-        add_row(gout + gi * T, !(GS && base == 0 && a.gmask0 && a.gmask0[gi] == 0));
+        add_row(gout + gi * T, !(z && a.gmask0[gi] == 0));
       }
       return make_grad4(v0, v1, v2, v3);
     }
     // one reach row: the loaded values as they are (adding them to 0 would consume the load now)
-    const R* row = gout + (int64_t)ref * T;
-    if (vec4) {
+#ifndef DDR_EXP_GRAD_DUMMY
+#define DDR_EXP_GRAD_DUMMY 0  // timing experiment only: dL/drunoff read from a 256-KB L2-resident window (wrong values)
+#endif
+    if (DDR_EXP_GRAD_DUMMY) {
+      const R* dm = gout + ((int64_t)(ref & 1023) << 6);
+      base &= 60;
       if constexpr (sizeof(R) == 4) {
-        const float4 v = *reinterpret_cast<const float4*>(row + base);
+        const float4 v = *reinterpret_cast<const float4*>(dm + base);
+        return make_grad4(v.x, v.y, v.z, v.w);
+      }
+    }
+    const R* row = gout + (int64_t)ref * T;
+    if (v4) {
+      if constexpr (sizeof(R) == 4) {
+        const float4 v = load_grad4(row + base);
         return make_grad4(v.x, v.y, v.z, v.w);
       } else {
         const double2 u = reinterpret_cast<const double2*>(row + base)[0];
@@ -1306,12 +1361,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         return make_grad4(u.x, u.y, w.x, w.y);
       }
     }
-    return make_grad4(row[base], row[i1], row[i2], row[i3]);
+    return make_grad4(row[i0], row[i1], row[i2], row[i3]);
   };
-  // ... plus the state seeds of steps T - 1 and T - 2 (a.gseed; a scalar test per group otherwise)
-  auto load_grad = [&](int ref, int64_t base, int gs) {
-    Grad4<R> v = load_grad_out(ref, base, gs);
-    if (a.gseed != nullptr && base + 3 >= T - 2) {
+  // ... plus the state seeds of steps T - 1 and T - 2 (a.gseed).  Only outside the steady ticks (seeded: the
+  // steady range then starts late enough that no steady tick loads the groups of those steps), so the steady
+  // loop's code and registers are those of an unseeded launch
+  auto load_grad = [&](int ref, int64_t base, int gs, bool seeded) {
+    Grad4<R> v = load_grad_out(ref, base, gs, seeded);
+    if (seeded && a.gseed != nullptr && base + 3 >= T - 2) {
       const R* sd = static_cast<const R*>(a.gseed);
       const R s1 = sd[ref], s2 = sd[a.N + ref];
       auto add = [&](R& g, int64_t t) { g = g + (t == T - 1 ? s1 : (t == T - 2 ? s2 : R(0))); };
@@ -1458,29 +1515,38 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       R sxv = R(0) + x0;
       sxv = sxv + x1;
       R I = R(0);
-      I = I + (nup > 0 ? (c0 ? x0 : rmax(x0, cs.qlb)) : R(0));
-      I = I + (nup > 1 ? (c0 ? x1 : rmax(x1, cs.qlb)) : R(0));
+      I = I + (nup > 0 ? (c0 ? x0 : rmaxc(x0, cs.qlb, cs)) : R(0));
+      I = I + (nup > 1 ? (c0 ? x1 : rmaxc(x1, cs.qlb, cs)) : R(0));
       if (nup > 2) {
         const int* lst = xl + up_f1(up[k]);
         const int c = lst[0];
         for (int j = 2; j < c; ++j) {
           const R xj = sxr[lst[j]];
           sxv = sxv + xj;
-          I = I + (c0 ? xj : rmax(xj, cs.qlb));
+          I = I + (c0 ? xj : rmaxc(xj, cs.qlb, cs));
         }
       }
       P.I = I;
       P.Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
       sxn[k] = sxv;
-      const int e4 = P.t & 3;
-      P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+      if constexpr (kShiftG) {
+        // dL/drunoff[:, t]: the group's registers shift by one step per tick (g3 holds step t: a group is loaded
+        // the tick before its top step runs) -- no per-lane select on t & 3
+        P.gk = g3[k];
+        g3[k] = g2[k];
+        g2[k] = g1[k];
+        g1[k] = g0[k];
+      } else {
+        const int e4 = P.t & 3;
+        P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+      }
       P.xtk = xc[k];
       P.st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(P.rs);
       P.lm = lam[k] + P.gk;                                 // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (P.xtk >= cs.qlb) ? P.lm : R(0);         // clamp backward (inclusive)
       P.gb64 = (double)gx + (double)A[k];                   // (I - C1 N)^T gb = gx (utils.py:188-242)
       P.gb = R(P.gb64);
-      P.Qp = c0 ? xa[k] : rmax(xa[k], cs.qlb);              // Q_{t-1}
+      P.Qp = c0 ? xa[k] : rmaxc(xa[k], cs.qlb, cs);              // Q_{t-1}
     };
     auto adjoint = [&](int k, const Pre& P, AdjOutR<R>& o) {
       if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
@@ -1491,7 +1557,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         R tw, ss;
         Geom<R> geo;
         coefficients<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, o.c1, o.c2, o.c3, o.c4, tw, ss, &geo);
-        const R qc = rmax(qvk, cs.qlb);
+        const R qc = rmaxc(qvk, cs.qlb, cs);
         const R gc1 = P.gb * P.Sx, gc2 = P.gb * P.I, gc3 = P.gb * P.Qp, gc4 = P.gb * qc;
         coefficients_vjp<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, geo, o.c1, o.c2, o.c3, o.c4, gc1, gc2, gc3, gc4, o.gQ, o.gn,
                                             o.gq, o.gp);
@@ -1543,7 +1609,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = P.t - 1;
       if (P.hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
-        const Grad4<R> v = load_grad(ref[k], (int64_t)(tn & ~3), kGReg ? opq(gsg[kGReg ? k : 0]) : -1);
+        const Grad4<R> v = load_grad(ref[k], kShiftG ? (int64_t)tn - 3 : (int64_t)(tn & ~3),
+                                     kGReg ? opq(gsg[kGReg ? k : 0]) : -1, !kSt);
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
       }
     };
@@ -1646,7 +1713,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
   for (int k = 0; k < KR; ++k)
     if (tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
-      const Grad4<R> v = load_grad(ref[k], (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1);
+      const Grad4<R> v = load_grad(ref[k], kShiftG ? T - 4 : (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1, true);
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
   if ((imp_mode || xhelp) && wbase >= BS / 2) {
@@ -1728,7 +1795,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   using Gen = std::integral_constant<bool, false>;
   using Steady = std::integral_constant<bool, true>;
   // steady backward ticks [b0, b1): forward ticks tau = TT - 1 - tb in [dmax + 2, T - 1]
-  int b0 = B.dmax, b1 = (int)T - 2;
+  // (state seeds: from forward tick T - 2 down, so that every load of the groups of steps T - 2 and T - 1 --
+  // issued at forward ticks >= T - 1 -- runs in a general tick)
+  int b0 = a.gseed != nullptr ? B.dmax + 1 : B.dmax, b1 = (int)T - 2;
   if (kEarly) {  // even bounds: the register roles keep alternating
     b0 += b0 & 1;
     b1 &= ~1;
