@@ -125,6 +125,30 @@ class ParamNet(torch.nn.Module):
         return torch.sigmoid(lin(self.layers[-1], x))
 
 
+class FusedNet:
+    """C3's parameter network as bench.py uses it: ``--pnet fused`` (default) is ddr_amd.pnet.ParamNet (the same
+    architecture and initialisation as ParamNet, forward + backward in two HIP launches, denormalisation fused);
+    ``--pnet torch`` is ParamNet + denorm in PyTorch ops.  Both return denormalised (n, q_spatial, p_spatial)."""
+
+    def __init__(self, kind, dev):
+        if kind == "fused":
+            from ddr_amd.pnet import ParamNet as Fused
+
+            self.net = Fused(10, RANGES).to(dev)
+        else:
+            self.net = ParamNet().to(dev)
+        self.kind = kind
+
+    def parameters(self):
+        return self.net.parameters()
+
+    def __call__(self, feats):
+        if self.kind == "fused":
+            return self.net(feats)
+        un = self.net(feats)
+        return denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
+
+
 def denorm(un, uq, up):
     """utils.py:166-185 (torch, autograd reaches the unit-interval parameters)."""
     n = un * (RANGES["n"][1] - RANGES["n"][0]) + RANGES["n"][0]
@@ -171,6 +195,18 @@ def cpu_baseline(args, net_global, x_const):
     out = {"value": rs / el, "unit": "reach-timesteps/s", "cores": 1, "nproc": os.cpu_count(), "kind": "port",
            "sample": f"{sample.n} reaches x {T} h {w.upper()}-shaped sample, {what}, {el:.1f} s",
            "forward_only_value": rs / t_fwd}
+    # basin-parallel: one single-threaded port process per core over disjoint C5-shaped basins (SURVEY §8(d)'s
+    # stronger CPU figure); the process count is the GPU's share of this box's cores (at most 16 per GPU here)
+    if w == "c5" and args.cpu_procs > 1:
+        from oracle.cpu_bench import basin_parallel
+
+        mp = basin_parallel(args.cpu_procs, args.cpu_reaches, max(1, args.basins * args.cpu_reaches // args.reaches),
+                            args.largest, T, grad, x_const, RANGES)
+        out["multi_process_value"] = mp["value"]
+        out["multi_process"] = {"processes": mp["processes"], "cores": mp["processes"], "wall_s": round(mp["wall_s"], 1),
+                                "per_process_value": mp["per_process_value"],
+                                "sample": f"{mp['processes']} disjoint {args.cpu_reaches}-reach x {T} h C5-shaped "
+                                          f"samples (seeds 100..), one single-threaded process each, {what}"}
     # the reference itself cannot travel to this box: its speed relative to the port was measured on the
     # same sample in the build container (tools/calibrate_cpu.py -> profiles/cpu_calibration.json, both on
     # one core); the reference-equivalent rate here is the port's rate divided by that ratio
@@ -318,6 +354,8 @@ def main():
     ap.add_argument("--warmup-days", type=int, default=3)
     ap.add_argument("--cpu-reaches", type=int, default=40_000)
     ap.add_argument("--cpu-T", type=int, default=720)
+    ap.add_argument("--cpu-procs", type=int, default=16,
+                    help="C5: also time this many port processes in parallel over disjoint basins (0/1: off)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dropin-steps", type=int, default=2, help="C5, 1 GPU: also time the drop-in dmc() path")
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
@@ -331,6 +369,8 @@ def main():
     ap.add_argument("--stream-builder", default="inline", choices=["inline", "device", "host"],
                     help="where the per-batch graph is built: on the device (ddr_graph_build_device, one builder "
                          "thread on its own stream) or on host threads (ddr_graph_build + upload)")
+    ap.add_argument("--pnet", default="fused", choices=["fused", "torch"],
+                    help="C3 parameter network: fused HIP kernels (ddr_amd.pnet) or the same network in PyTorch ops")
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
     ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
@@ -431,7 +471,7 @@ def main():
         from ddr_amd.distributed import allreduce_gradients
 
         feats = tt(synthetic.reach_features(net.n, seed=11))
-        model = ParamNet().to(dev)
+        model = FusedNet(args.pnet, dev)
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)  # one launch per step, not per tensor
         # one gauge per subnetwork outlet; observations indexed by the gauge's global number
         outlets_global = np.flatnonzero(net.down < 0)
@@ -445,8 +485,7 @@ def main():
 
         def step():
             opt.zero_grad(set_to_none=True)
-            un = model(feats)
-            n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
+            n, q, p = model(feats)
             daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
                                    math=args.math, steps=T, qprime_hours=qp_hours)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
@@ -568,6 +607,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {"workload": spec["desc"] + (" + dL/dq' (state-gradient adjoint)" if args.grad_qprime else ""), "reaches": total_reaches, "T": T, "qprime_store": "daily" if qp_hours == 24 else "hourly",
+                       "parameter_network": ({"fused": "fused HIP MLP 10-128-128-128-3 (ddr_amd.pnet, fp32 MFMA)",
+                                              "torch": "PyTorch MLP 10-128-128-128-3"}[args.pnet]
+                                             if args.workload == "c3" else None),
                        "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",
                                         "faithful": "faithful (reference op order, IEEE division, fp32 faithful-class pow)",
                                         "fast": "fast (hardware rcp/log/exp fp32)"}[args.math],
@@ -643,7 +685,7 @@ def time_training_stream(args, dev):
                                               (len(outlets), window.D)).astype(np.float32)).to(dev)))
     log(f"[stream] {M} batches resident in {time.perf_counter() - t_gen:.1f}s "
         f"({min(d['net'].n for d in data)}..{max(d['net'].n for d in data)} reaches)")
-    model = ParamNet().to(dev)
+    model = FusedNet(args.pnet, dev)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     wd = args.warmup_days
     consts = RouteConsts()
@@ -676,8 +718,7 @@ def time_training_stream(args, dev):
         e0.record()
         d = data[m]
         opt.zero_grad(set_to_none=True)
-        un = model(d["feats"])
-        n, q, p = denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
+        n, q, p = model(d["feats"])
         daily, _, _, _ = route(g, d["qprime"], n, q, p, d["length"], d["slope"], d["xs"], gauges=d["gz"],
                                daily=window, consts=consts, steps=T, qprime_hours=24, math=args.math)
         loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])

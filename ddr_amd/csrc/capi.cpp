@@ -486,6 +486,31 @@ ddr_status gauge_daily_seed_impl(int64_t G, int64_t T, int64_t t0, int64_t L, in
     return fail(DDR_ERR_ARG, "internal error");          \
   }
 
+ddr_status pnet_forward_impl(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                             const float* denorm, float* z_save, float* u_save, float* out_n, float* out_q,
+                             float* out_p, void* stream) {
+  if (n_rows < 0 || n_features < 1 || n_features > 12) return fail(DDR_ERR_ARG, "pnet: 0 <= rows, 1 <= features <= 12");
+  if (n_rows > 0 && (!x || !params || !denorm || !z_save || !u_save || !out_n || !out_q || !out_p))
+    return fail(DDR_ERR_ARG, "pnet: null argument");
+  if (n_rows >= (int64_t(1) << 31) / 64 * 64) return fail(DDR_ERR_ARG, "pnet: too many rows");
+  float* out[3] = {out_n, out_q, out_p};
+  DDR_HIP(launch_pnet_forward(n_rows, n_features, x, params, denorm, z_save, u_save, out, static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+ddr_status pnet_backward_impl(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                              const float* denorm, const float* z_save, const float* u_save, const float* grad_n,
+                              const float* grad_q, const float* grad_p, float* grad_params, void* work, void* stream) {
+  if (n_rows < 0 || n_features < 1 || n_features > 12) return fail(DDR_ERR_ARG, "pnet: 0 <= rows, 1 <= features <= 12");
+  if (!grad_params || !params || !denorm) return fail(DDR_ERR_ARG, "pnet: null argument");
+  if (n_rows > 0 && (!x || !z_save || !u_save || !grad_n || !grad_q || !grad_p || !work))
+    return fail(DDR_ERR_ARG, "pnet: null argument");
+  if (n_rows >= (int64_t(1) << 31) / 64 * 64) return fail(DDR_ERR_ARG, "pnet: too many rows");
+  const float* g[3] = {grad_n, grad_q, grad_p};
+  DDR_HIP(launch_pnet_backward(n_rows, n_features, x, params, denorm, z_save, u_save, g, grad_params, work,
+                               static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+
 template <typename R>
 ddr_status state_impl(const ddr_graph* gh, const R* x_save, int64_t T, int64_t t, double qlb, int32_t flags, R* out,
                       void* stream) {
@@ -974,6 +999,25 @@ ddr_status ddr_mc_backward_ex_f64(const ddr_graph* g, const ddr_mc_consts* c, co
   DDR_GUARD({ return backward_impl<double>(g, c, r, qprime, T, x_save, bnd, grad, gauges, bwd_bnd, status, gn, gq, gp, flags, stream, qprime_rows, grad_qprime, grad_q0, work, state_seed); })
 }
 
+int64_t ddr_pnet_param_count(int32_t n_features) {
+  if (n_features < 1 || n_features > 12) return -1;
+  return pnet_param_count(n_features);
+}
+int64_t ddr_pnet_work_bytes(int64_t n_rows, int32_t n_features) {
+  if (n_rows < 0 || n_features < 1 || n_features > 12) return -1;
+  return pnet_work_bytes(n_rows, n_features);
+}
+ddr_status ddr_pnet_forward_f32(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                                const float* denorm, float* z_save, float* u_save, float* out_n, float* out_q,
+                                float* out_p, void* stream) {
+  DDR_GUARD({ return pnet_forward_impl(n_rows, n_features, x, params, denorm, z_save, u_save, out_n, out_q, out_p, stream); })
+}
+ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                                 const float* denorm, const float* z_save, const float* u_save, const float* grad_n,
+                                 const float* grad_q, const float* grad_p, float* grad_params, void* work,
+                                 void* stream) {
+  DDR_GUARD({ return pnet_backward_impl(n_rows, n_features, x, params, denorm, z_save, u_save, grad_n, grad_q, grad_p, grad_params, work, stream); })
+}
 ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
                          int32_t flags, float* out, void* stream) {
   DDR_GUARD({ return state_impl<float>(g, x_save, T, t, discharge_lb, flags, out, stream); })

@@ -145,6 +145,13 @@ hipError_t launch_gauge_daily(const GaugeArgs& a, const R* xsave, int64_t t0, in
 template <typename R>
 hipError_t launch_gauge_daily_seed(int64_t G, int64_t T, int64_t t0, int64_t L, int64_t D, const R* gd, R* gh,
                                    hipStream_t stream);
+// pnet.hip: the fused parameter network (C3's KAN stand-in); denorm = host [3][3] (scale, offset, log flag)
+int pnet_param_count(int F);
+int64_t pnet_work_bytes(int64_t N, int F);
+hipError_t launch_pnet_forward(int64_t N, int F, const float* X, const float* P, const float* denorm, float* Z, float* U,
+                               float* const out[3], hipStream_t stream);
+hipError_t launch_pnet_backward(int64_t N, int F, const float* X, const float* P, const float* denorm, const float* Z,
+                                const float* U, const float* const gout[3], float* grad, void* work, hipStream_t stream);
 // geometry.hip: windows of up to kGeoLongMaxDays days (~89 years; beyond 512 days one workgroup per
 // reach sorts each variable in LDS)
 constexpr int64_t kGeoLongMaxDays = 32768;

@@ -333,6 +333,28 @@ ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int
 ddr_status ddr_state_f64(const ddr_graph* g, const double* x_save, int64_t T, int64_t t, double discharge_lb,
                          int32_t flags, double* out, void* stream);
 
+/* Fused parameter network of the C3 training step (the bench's stand-in for the reference's KAN,
+ * src/ddr/nn/kan.py:11-62, whose pykan dependency is not installed): attributes x (n_rows, n_features <= 12)
+ * -> Linear(F, 128) -> SiLU -> Linear(128, 128) -> SiLU -> Linear(128, 128) -> SiLU -> Linear(128, 3) -> sigmoid
+ * -> denormalize (routing/utils.py:166-185: y = u scale + offset, exp(y) for a log-space parameter) ->
+ * out_n, out_q, out_p (n_rows each), on the fp32 matrix cores.
+ *   params  flat fp32, ddr_pnet_param_count(F) values: W1 (128, F) | b1 (128) | W2 (128, 128) | b2 | W3 | b3 |
+ *           W4 (3, 128) | b4 (3), torch.nn.Linear's (out, in) weight layout
+ *   denorm  HOST array [3][3]: per output (scale, offset, log-space flag)
+ *   z_save  (3, n_rows, 128) pre-activations, u_save (n_rows, 3) sigmoid outputs: kept for the backward
+ *   grad_params (same layout as params) = dL/dparams given dL/d(out_n, out_q, out_p); work: device scratch of
+ *           ddr_pnet_work_bytes bytes.  Deterministic (fixed-order reduction of per-workgroup partials).
+ * Replaces: the network's forward (kan.py:50-62) and its torch autograd in scripts/train.py:54-104. */
+int64_t ddr_pnet_param_count(int32_t n_features);
+int64_t ddr_pnet_work_bytes(int64_t n_rows, int32_t n_features);
+ddr_status ddr_pnet_forward_f32(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                                const float* denorm, float* z_save, float* u_save, float* out_n, float* out_q,
+                                float* out_p, void* stream);
+ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float* x, const float* params,
+                                 const float* denorm, const float* z_save, const float* u_save, const float* grad_n,
+                                 const float* grad_q, const float* grad_p, float* grad_params, void* work,
+                                 void* stream);
+
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,

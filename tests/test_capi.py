@@ -38,3 +38,13 @@ def test_version_and_error_plumbing():
     code = lib.ddr_graph_build(0, 0, None, None, None, C.byref(C.c_void_p()))
     assert code == _lib.DDR_ERR_ARG
     assert b"at least one reach" in lib.ddr_last_error()
+
+
+def test_pnet_param_count_matches_python():
+    from ddr_amd import _lib
+    from ddr_amd.pnet import param_count
+
+    lib = _lib.load()
+    for F in (1, 7, 10, 12):
+        assert int(lib.ddr_pnet_param_count(F)) == param_count(F)
+    assert int(lib.ddr_pnet_param_count(13)) == -1

@@ -10,8 +10,9 @@ for size in ${WLS:-light c5}; do
     case $size in
       light) fl="--reaches 100000 --basins 400";;
       c5) fl="";;
-      c3s8) fl="--workload c3"; envs="WORLD_SIZE=8 RANK=1 DDR_BENCH_ALONE=1";;  # one 8-way C3 shard alone
+      c3s8) fl="--workload c3 $C3FL"; envs="WORLD_SIZE=8 RANK=1 DDR_BENCH_ALONE=1";;  # one 8-way C3 shard alone
       c5s8) fl=""; envs="WORLD_SIZE=8 RANK=0 DDR_BENCH_ALONE=1";;               # the giant-basin C5 shard
+      c3) fl="--workload c3 $C3FL";;
       *) fl="--workload $size";;
     esac
     env $envs DDR_MC_LIB=$lib timeout -k 10 300 python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --dropin-steps ${DROPIN:-0} $fl > $OUT/${v}_$size.log 2>&1 || { echo "$v $size failed"; tail -3 $OUT/${v}_$size.log; exit 1; }
