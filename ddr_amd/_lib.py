@@ -39,6 +39,7 @@ DDR_FWD_ACCUMULATE = 8
 DDR_FWD_FAST_MATH = 16
 DDR_FWD_FAITHFUL_MATH = 32
 DDR_FWD_CHECK_QPRIME = 64
+DDR_BWD_EXACT_ADJOINT = 128
 
 DDR_DEBUG_FORCE_TIMEOUT = 1
 DDR_DEBUG_NO_STEADY = 2

@@ -447,13 +447,21 @@ __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, c
 // ---- fp32 adjoint step (backward kernel, fp32 build): the step's physics recomputed in hardware
 // fp32 math and its VJP, folded algebraically.  Equivalent in exact arithmetic to
 // coefficients<float, true> + coefficients_vjp<float, true>; per reach-step ~15 transcendental and
-// ~90 other instructions.  Uses x(t) = c1 Sx + c2 I + c3 Q + c4 qc (the forward solve) to collapse
-// sum_k gc_k c_k into gb x.
+// ~90 other instructions.
+// dL/d(2k) = sum_k gc_k dc_k/d(2k) is a sum of O(Q) terms that cancels to O(dQ/dt) (its exact value is
+// gb / den [X (I - Sx) + (1 - X)(Q - x~)], x~ = c1 Sx + c2 I + c3 Q + c4 qc).  With c1 + c2 = c4 = 1 - c3 it is
+//   gb / den [D1 (X + (1 - X) c1) + D2 ((1 - X) c2 - X)],   D1 = Q - qc - Sx,  D2 = Q - qc - I,
+// where the coefficients multiply the step's mass imbalances D1, D2 (DF: formed exactly in fp64 by the caller
+// from the fp32 states; a1 = D1, a2 = D2), so their ~1e-6 recompute error stays ~1e-6 of the result.  The default
+// (a1 = x(t), a2 = Sx, a3 = I) takes Q - x~ from the stored fp32 x(t) -- no q' re-read -- which carries the
+// forward's rounding of x (~1e-7 Q) into a quantity of size dQ: 1.6e-3 / 4.7e-3 / 2.4e-3 of the gradient on a
+// 2215-deep basin, ~1e-7 on shallow trees (tools/grad_terms.py; DDR_BWD_EXACT_ADJOINT).
 struct AdjOut {
   float c1, c2, c3, c4, gQ, gn, gq, gp;
 };
+template <bool DF>
 __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s, float Q, const Consts<float>& c,
-                                                    float gb, float x, float Sx, float I) {
+                                                    float gb, float a1, float a2, float a3) {
   constexpr float kLn2 = 0.69314718055994530942f;
   const float qe = s.qe, qe1 = qe + 1.0f, expo = s.expo;
   // ---- recompute (geometry/trapezoidal.py:62-97, routing/mmc.py:165-167, 479-484) ----
@@ -494,8 +502,9 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
   const float c4 = (2.0f * c.dt) * rden;
   o.c3 = 1.0f - c4;
   o.c4 = c4;
-  // ---- VJP: gc = gb (Sx, I, Q, qc); sum_k gc_k c_k = gb x ----
-  const float g_twok = gb * fmaf(s.X, I - Sx, omX * (Q - x)) * rden;
+  // ---- VJP: gc = gb (Sx, I, Q, qc) ----
+  const float g_twok = DF ? (gb * fmaf(a1, fmaf(omX, o.c1, s.X), a2 * fmaf(omX, o.c2, -s.X))) * rden
+                          : gb * fmaf(s.X, a3 - a2, omX * (Q - a1)) * rden;
   const float g_cel = -(g_twok * twok) * rcel;                    // k = L / cel
   const bool vin = (v >= c.vlb) && (v <= c.vub);
   const float gvv = vin ? (g_cel * (5.0f / 3.0f)) * v : 0.0f;     // dL/d ln v
@@ -542,8 +551,9 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
 
 // adjoint_step_fast of two reaches at once (packed halves; the same operations, so the same bits).
 struct AdjIn {
-  float Q, gb, x, Sx, I;
+  float Q, gb, a1, a2, a3;  // adjoint_step_fast's
 };
+template <bool DF>
 __device__ __forceinline__ void adjoint_step_fast2(const ReachStatic<float>& s0, const ReachStatic<float>& s1,
                                                    const AdjIn& i0, const AdjIn& i1, const Consts<float>& c, AdjOut& o0,
                                                    AdjOut& o1) {
@@ -554,7 +564,7 @@ __device__ __forceinline__ void adjoint_step_fast2(const ReachStatic<float>& s0,
   auto ex = [](f2 a) { return mk2(__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)); };
   auto mx = [](f2 a, float lo) { return mk2(rmax(a.x, lo), rmax(a.y, lo)); };
   auto cl = [](f2 a, float lo, float hi) { return mk2(rclamp(a.x, lo, hi), rclamp(a.y, lo, hi)); };
-  const f2 Q = pr(i0.Q, i1.Q), gb = pr(i0.gb, i1.gb), x = pr(i0.x, i1.x), Sx = pr(i0.Sx, i1.Sx), I = pr(i0.I, i1.I);
+  const f2 Q = pr(i0.Q, i1.Q), gb = pr(i0.gb, i1.gb), U = pr(i0.a1, i1.a1), V = pr(i0.a2, i1.a2), W = pr(i0.a3, i1.a3);
   const f2 qe = pr(s0.qe, s1.qe), qe1 = qe + sp2(1.0f), expo = pr(s0.expo, s1.expo);
   const f2 n = pr(s0.n, s1.n), p = pr(s0.p, s1.p), inv_n = pr(s0.inv_n, s1.inv_n), sqrtS = pr(s0.sqrtS, s1.sqrtS);
   const f2 L = pr(s0.L, s1.L), X = pr(s0.X, s1.X);
@@ -595,7 +605,8 @@ __device__ __forceinline__ void adjoint_step_fast2(const ReachStatic<float>& s0,
   const f2 c4 = sp2(2.0f * c.dt) * rden;
   const f2 c3 = sp2(1.0f) - c4;
   // ---- VJP ----
-  const f2 g_twok = gb * fma2(X, I - Sx, omX * (Q - x)) * rden;
+  const f2 g_twok = DF ? (gb * fma2(U, fma2(omX, c1, X), V * fma2(omX, c2, -X))) * rden
+                       : gb * fma2(X, W - V, omX * (Q - U)) * rden;
   const f2 g_cel = -(g_twok * twok) * rcel;
   const f2 gvc = (g_cel * sp2(5.0f / 3.0f)) * v;
   const f2 gvv = mk2((v.x >= c.vlb && v.x <= c.vub) ? gvc.x : 0.0f, (v.y >= c.vlb && v.y <= c.vub) ? gvc.y : 0.0f);

@@ -1108,7 +1108,7 @@ __device__ __forceinline__ Grad4<R> make_grad4(R a, R b, R c, R d) { return Grad
 // of every step (gb c4 [q' >= q_lb], mmc.py:421-424, 535-538) into gqs, the schedule layout of qs.
 // XB: the slot buffers when not the KR rule's (bwd_xbuf): 1 = single-buffered slots where the double buffer
 // does not fit the LDS (fp64 at KR = 2, bwd_xb_of)
-template <typename R, int KR, bool GS, int XB = 0>
+template <typename R, int KR, bool GS, int XB = 0, bool DF = false>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1156,7 +1156,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // xc = x(t), xa = x(t-1), xb = x(t-2) (published this tick, then reloaded with x(t-3), while
   // x(t-2) stays readable in the reach's own slot); sxn = sum_j x_j(t) (upstream);
   // g0..g3: dL/drunoff of the four steps of t's group (t & ~3 .. t | 3)
-  R lam[KR], xc[KR], xa[KR], xb[KR], sxn[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  R lam[KR], xc[KR], xa[KR], xb[KR], pn[KR], pq[KR], pp[KR], g0[KR], g1[KR], g2[KR], g3[KR];
+  // kDF (DDR_BWD_EXACT_ADJOINT, fp32 fast adjoint): the step's mass imbalances D1 = Q - qc - Sx, D2 = Q - qc - I
+  // formed in fp64 from the fp32 states (physics.h adjoint_step_fast): the upstream sums carried in fp64, qc
+  // re-read.  Else X (I - Sx) + (1 - X)(Q - x~) with x~ := x(t), the stored state
+  constexpr bool kDF = DF && std::is_same<R, float>::value && !DDR_BWD_EXACT;
+#ifndef DDR_EXP_DF_F32
+#define DDR_EXP_DF_F32 0
+#endif
+#ifndef DDR_EXP_DF_NOQ
+#define DDR_EXP_DF_NOQ 0
+#endif
+  using SxT = typename std::conditional<kDF && !DDR_EXP_DF_F32, double, R>::type;
+  SxT sxn[KR];
   // the gradient groups as shift registers (KR <= 2: c3s8 backward -4 %); at KR = 4 the select on t & 3 measured
   // faster (C5 backward 59.5 vs 57.3 ms, profiles/r05/ab_r05.txt)
 #ifndef DDR_BWD_SHIFT_MAX_KR
@@ -1173,7 +1185,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // three dependent loads each followed by a wait
   constexpr bool kGReg = KR <= 2;
   int gsg[kGReg ? KR : 1];
-  R qsv[GS ? KR : 1];  // state gradients: q' * flow_scale of this tick's step (prefetched a tick ahead)
+  constexpr bool kQs = GS || (kDF && !DDR_EXP_DF_NOQ);
+  R qsv[kQs ? KR : 1];  // q' * flow_scale of this tick's step (prefetched a tick ahead): state gradients, kDF
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
   ReachStatic<R> sreg[kStatReg ? KR : 1];
@@ -1195,7 +1208,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     }
     od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu) | (nograd ? 0x80000000u : 0u);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
-    lam[k] = sxn[k] = R(0);
+    lam[k] = R(0);
+    sxn[k] = SxT(0);
     xc[k] = xa[k] = xb[k] = R(0);
     pn[k] = pq[k] = pp[k] = R(0);
     g0[k] = g1[k] = g2[k] = g3[k] = R(0);
@@ -1495,7 +1509,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     struct Pre {
       int r, rs, t;
       bool hk, active, c0;
-      R Sx, I, gk, xtk, lm, gb, Qp;
+      R Sx, I, gk, xtk, lm, gb, Qp, D1, D2;
       double gb64;
       ReachStatic<R> st;
     };
@@ -1512,22 +1526,23 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       const int nup = up_n(up[k]);
       const R x0 = sxr[up_0(up[k])];
       const R x1 = sxr[up_1(up[k], xl)];
-      R sxv = R(0) + x0;
-      sxv = sxv + x1;
-      R I = R(0);
-      I = I + (nup > 0 ? (c0 ? x0 : rmaxc(x0, cs.qlb, cs)) : R(0));
-      I = I + (nup > 1 ? (c0 ? x1 : rmaxc(x1, cs.qlb, cs)) : R(0));
+      SxT sxv = SxT(0) + SxT(x0);
+      sxv = sxv + SxT(x1);
+      SxT I = SxT(0);
+      I = I + SxT(nup > 0 ? (c0 ? x0 : rmaxc(x0, cs.qlb, cs)) : R(0));
+      I = I + SxT(nup > 1 ? (c0 ? x1 : rmaxc(x1, cs.qlb, cs)) : R(0));
       if (nup > 2) {
         const int* lst = xl + up_f1(up[k]);
         const int c = lst[0];
         for (int j = 2; j < c; ++j) {
           const R xj = sxr[lst[j]];
-          sxv = sxv + xj;
-          I = I + (c0 ? xj : rmaxc(xj, cs.qlb, cs));
+          sxv = sxv + SxT(xj);
+          I = I + SxT(c0 ? xj : rmaxc(xj, cs.qlb, cs));
         }
       }
-      P.I = I;
-      P.Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
+      const SxT Sx = sxn[k];  // sum_j x_j(t), the solve's upstream term of this step
+      P.I = R(I);
+      P.Sx = R(Sx);
       sxn[k] = sxv;
       if constexpr (kShiftG) {
         // dL/drunoff[:, t]: the group's registers shift by one step per tick (g3 holds step t: a group is loaded
@@ -1547,10 +1562,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       P.gb64 = (double)gx + (double)A[k];                   // (I - C1 N)^T gb = gx (utils.py:188-242)
       P.gb = R(P.gb64);
       P.Qp = c0 ? xa[k] : rmaxc(xa[k], cs.qlb, cs);              // Q_{t-1}
+      if constexpr (kDF) {
+        const SxT Qq = (SxT)P.Qp - (SxT)(DDR_EXP_DF_NOQ ? R(0) : rmaxc(qsv[kQs ? k : 0], cs.qlb, cs));  // exact in fp64
+        P.D1 = R(Qq - Sx);
+        P.D2 = R(Qq - I);
+      }
     };
     auto adjoint = [&](int k, const Pre& P, AdjOutR<R>& o) {
       if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
-        const AdjOut f = adjoint_step_fast(P.st, P.Qp, cs, P.gb, P.xtk, P.Sx, P.I);
+        AdjOut f;
+        if constexpr (kDF) f = adjoint_step_fast<true>(P.st, P.Qp, cs, P.gb, P.D1, P.D2, R(0));
+        else f = adjoint_step_fast<false>(P.st, P.Qp, cs, P.gb, P.xtk, P.Sx, P.I);
         o = AdjOutR<R>{f.c1, f.c2, f.c3, f.c4, f.gQ, f.gn, f.gq, f.gp};
       } else {
         const R qvk = *qs_at<R>(a, B, xs_base, tau, off_of(k), P.rs);  // q'[t-1] * flow_scale
@@ -1602,7 +1624,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     };
     auto tail = [&](int k, const Pre& P) {
-      if constexpr (GS) {
+      if constexpr (kQs) {
         const int tn = tau > 0 ? tau - 1 : 0;  // the next backward tick's row
         qsv[k] = *qs_at<R>(a, B, xs_base, tn, off_of(k), P.rs);
       }
@@ -1631,8 +1653,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if constexpr (NPB == 2) {
           // two slices' adjoint steps in packed halves (the same bits as two scalar steps)
           AdjOut f0, f1;
-          adjoint_step_fast2(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].xtk, P[0].Sx, P[0].I},
-                             AdjIn{P[1].Qp, P[1].gb, P[1].xtk, P[1].Sx, P[1].I}, cs, f0, f1);
+          if constexpr (kDF)
+            adjoint_step_fast2<true>(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].D1, P[0].D2, 0.0f},
+                                     AdjIn{P[1].Qp, P[1].gb, P[1].D1, P[1].D2, 0.0f}, cs, f0, f1);
+          else
+            adjoint_step_fast2<false>(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].xtk, P[0].Sx, P[0].I},
+                                      AdjIn{P[1].Qp, P[1].gb, P[1].xtk, P[1].Sx, P[1].I}, cs, f0, f1);
           o[0] = AdjOutR<R>{f0.c1, f0.c2, f0.c3, f0.c4, f0.gQ, f0.gn, f0.gq, f0.gp};
           o[1] = AdjOutR<R>{f1.c1, f1.c2, f1.c3, f1.c4, f1.gQ, f1.gn, f1.gq, f1.gp};
         } else {
@@ -1666,7 +1692,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   };
 
   // tick 0 runs forward tick TT-1: x(t) at row TT-1, x(t-1) at row TT-2, x(t-2) at row TT-3
-  if constexpr (GS) {
+  if constexpr (kQs) {
 #pragma unroll
     for (int k = 0; k < KR; ++k) {
       const int r = tid + k * BS;
@@ -1689,11 +1715,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
     if (r >= B.nloc) continue;
-    R v = R(0) + sxp[up_0(up[k])];
-    v = v + sxp[up_1(up[k], xl)];
+    SxT v = SxT(0) + SxT(sxp[up_0(up[k])]);
+    v = v + SxT(sxp[up_1(up[k], xl)]);
     if (up_n(up[k]) > 2) {
       const int* lst = xl + up_f1(up[k]);
-      for (int j = 2; j < lst[0]; ++j) v = v + sxp[lst[j]];
+      for (int j = 2; j < lst[0]; ++j) v = v + SxT(sxp[lst[j]]);
     }
     sxn[k] = v;
   }
@@ -2141,11 +2167,17 @@ size_t route_smem_bytes(const Graph* g, bool backward) {
 }
 
 // the backward kernel of this launch (state gradients: GS; single-buffered fp64 KR = 2 slots: bwd_xb_of)
+// (exact adjoint of the fp32 trajectory, DDR_BWD_EXACT_ADJOINT: df)
 template <typename R, int KR>
-const void* backward_kernel_of(const Graph* g, bool gs) {
+const void* backward_kernel_of(const Graph* g, bool gs, bool df = false) {
   if constexpr (KR == 2 && sizeof(R) == 8) {
     if (bwd_xb_of<R>(g) == 1)
       return gs ? (const void*)route_backward_kernel<R, KR, true, 1> : (const void*)route_backward_kernel<R, KR, false, 1>;
+  }
+  if constexpr (sizeof(R) == 4) {
+    if (df)
+      return gs ? (const void*)route_backward_kernel<R, KR, true, 0, true>
+                : (const void*)route_backward_kernel<R, KR, false, 0, true>;
   }
   return gs ? (const void*)route_backward_kernel<R, KR, true> : (const void*)route_backward_kernel<R, KR, false>;
 }
@@ -2162,7 +2194,7 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   a.xt_off = g->split.nranks > 0 ? (int32_t)align16(base) : 0;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
-    const void* kern = backward_kernel_of<R, KR>(g, a.gqs != nullptr);
+    const void* kern = backward_kernel_of<R, KR>(g, a.gqs != nullptr, (a.flags & DDR_BWD_EXACT_ADJOINT) != 0);
     hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     void* kargs[] = {&a};

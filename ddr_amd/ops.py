@@ -438,7 +438,7 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
           q0: torch.Tensor | None = None, gauges: GaugeMap | None = None, consts: RouteConsts = RouteConsts(),
           save: bool | None = None, steps: int | None = None, qprime_hours: int = 1,
           qprime_valid: torch.Tensor | None = None, daily: DailyWindow | None = None, accumulate: bool = False,
-          fast_math: bool = False, math: str | None = None, check_qprime: bool = False):
+          fast_math: bool = False, math: str | None = None, check_qprime: bool = False, exact_adjoint: bool = False):
     """Fused differentiable routing.  Returns (runoff, q_last, top_width_last, side_slope_last).
 
     ``math`` (fp32 forward): ``"exact"`` (default) -- the reference's operation order, IEEE division,
@@ -459,7 +459,13 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
 
     ``check_qprime``: the q' gather also tests the window's flow-scaled q' for NaN (the reference's
     cold-start assertion, mmc.py:335); :func:`qprime_has_nan` then returns the verdict, waiting for the
-    gather only."""
+    gather only.
+
+    ``exact_adjoint`` (fp32 backward): the gradients are the exact adjoint of the fp32 trajectory the forward
+    computed (~1e-7 norm-relative on any depth; the fp32 default is ~1e-3 on a 2215-deep basin, ~1e-7 on
+    shallow ones) at ~30 % more backward time (q' re-read, fp64 upstream sums: DDR_BWD_EXACT_ADJOINT).  The
+    fp64 model's own gradient differs from both by the fp32 states' rounding (~1e-3 there); route in fp64 for
+    that."""
     dt = qprime.dtype
     dev = qprime.device
 
@@ -479,7 +485,8 @@ def route(graph: RiverGraph, qprime: torch.Tensor, n: torch.Tensor, q: torch.Ten
     flags = ((_lib.DDR_FWD_SAVE_X if save else 0) | (_lib.DDR_FWD_CARRY if q0 is not None else 0)
              | (_lib.DDR_FWD_ACCUMULATE if accumulate else 0) | (_lib.DDR_FWD_FAST_MATH if math == "fast" else 0)
              | (_lib.DDR_FWD_FAITHFUL_MATH if math == "faithful" else 0)
-             | (_lib.DDR_FWD_CHECK_QPRIME if check_qprime else 0))
+             | (_lib.DDR_FWD_CHECK_QPRIME if check_qprime else 0)
+             | (_lib.DDR_BWD_EXACT_ADJOINT if exact_adjoint else 0))
     valid = None if qprime_valid is None else qprime_valid.to(device=dev, dtype=torch.uint8).contiguous()
     gid = register_graph(graph)
     gz = gauges

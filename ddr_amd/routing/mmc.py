@@ -134,6 +134,10 @@ class MuskingumCunge:
             raise ValueError(f"routing_math must be 'exact', 'faithful' or 'fast', not {self.math!r}")
         self._eager_nan_check = bool(getattr(cfg.params, "eager_nan_check", False)) or \
             os.environ.get("DDR_EAGER_NAN_CHECK") == "1"
+        # the fp32 backward as the exact adjoint of the fp32 trajectory (ops.route exact_adjoint; ~30 % more
+        # backward time): cfg.params.exact_adjoint or DDR_EXACT_ADJOINT=1
+        self._exact_adjoint = bool(getattr(cfg.params, "exact_adjoint", False)) or \
+            os.environ.get("DDR_EXACT_ADJOINT") == "1"
         self.t = torch.tensor(3600.0, device=self.device)
         self.n: torch.Tensor | None = None
         self.q_spatial: torch.Tensor | None = None
@@ -281,7 +285,8 @@ class MuskingumCunge:
         q0 = None if own else self._discharge_t
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
                                        self.slope, self.x_storage, q0=q0, gauges=self._gauges,
-                                       consts=self._consts(), math=self.math, check_qprime=own)
+                                       consts=self._consts(), math=self.math, check_qprime=own,
+                                       exact_adjoint=self._exact_adjoint)
         # mmc.py:335 (the cold start's assertion), decided by the launch's q' gather: this waits for the
         # gather only -- the routing kernel queued behind it keeps running while the host goes on
         assert not (own and qprime_has_nan()), "q_prime has NaN flows"
@@ -325,7 +330,7 @@ class MuskingumCunge:
         qp = torch.cat([q, q], 0)
         runoff, q_last, tw, ss = route(self._graph, qp, self.n, self.q_spatial, self._p_tensor(qp), self.length,
                                        self.slope, self.x_storage, q0=self._discharge_t, consts=self._consts(),
-                                       math=self.math)
+                                       math=self.math, exact_adjoint=self._exact_adjoint)
         self.top_width = _apply_data_override(tw, self._data_top_width)
         self.side_slope = _apply_data_override(ss, self._data_side_slope)
         return q_last

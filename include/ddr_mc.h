@@ -229,7 +229,13 @@ typedef struct {
  *   arithmetic (like the reference's own Sleef powf; no fp64 on the chain);
  * DDR_FWD_FAST_MATH: hardware v_rcp / v_log / v_exp throughout (~1e-6 relative per coefficient). */
 enum { DDR_FWD_SAVE_X = 1, DDR_FWD_CARRY = 2, DDR_FWD_NO_RUNOFF = 4, DDR_FWD_ACCUMULATE = 8, DDR_FWD_FAST_MATH = 16,
-       DDR_FWD_FAITHFUL_MATH = 32, DDR_FWD_CHECK_QPRIME = 64 };
+       DDR_FWD_FAITHFUL_MATH = 32, DDR_FWD_CHECK_QPRIME = 64, DDR_BWD_EXACT_ADJOINT = 128 };
+/* DDR_BWD_EXACT_ADJOINT (backward flag, fp32; ignored by the forward): the adjoint of the fp32 trajectory the
+ * forward computed to ~1e-6 on any depth.  dL/dk (the Muskingum K) is a sum of O(Q) terms that cancels to the
+ * step's discharge change; by default the fp32 adjoint takes that change as Q(t-1) - x(t) from the stored
+ * fp32 state (no q' re-read), which carries x's rounding into it: ~1e-3 of the gradient on a 2215-deep
+ * basin, ~1e-7 on shallow ones.  With the flag it forms the step's mass imbalances Q(t-1) - q'c - sum x_j(t)
+ * and Q(t-1) - q'c - I(t) exactly (fp64 upstream sums, q' re-read): 1.8e-7 there, +30 % backward time. */
 /* DDR_FWD_CHECK_QPRIME: the forward also tests the flow-scaled q' of the window for NaN (the reference's
  * cold-start assertion, mmc.py:335) inside its q' gather -- no extra pass over q'.  The verdict of the
  * calling thread's last such launch: ddr_qprime_nan_wait, which waits for the gather only (an event

@@ -40,7 +40,7 @@ __global__ void __launch_bounds__(1024) chain(int K, float* out, unsigned long l
     double x;
     if constexpr (MODE == 3) {
       const float Qk = Q + 1e-7f * (float)k;  // the saved state: off the chain
-      const AdjOut o = adjoint_step_fast(st, Qk, cs, gb, 0.9f * Qk, (float)xu, In);
+      const AdjOut o = adjoint_step_fast<false>(st, Qk, cs, gb, 0.9f * Qk, (float)xu, In);
       x = (double)(0.5f + o.gQ * 0.25f + o.gn * 1e-3f + o.gq * 1e-3f + o.gp * 1e-3f) + (double)o.c1 * xu;
     } else if constexpr (MODE == 4) {
       x = 0.999 * xu + (double)Q;

@@ -1,5 +1,9 @@
 """Gradient accuracy vs depth: the C5 giant basin (281k reaches, depth 2215) routed alone over a
-short horizon, fp32 kernel gradients vs the fp64 oracle adjoint (on the kernel's fp32 states).
+short horizon; the fp32 kernel's gradients against
+  n, q_spatial, p_spatial    the fp64 oracle adjoint on the oracle's own fp32 forward states
+  own:*                      the fp64 oracle adjoint on the kernel's fp32 states (its runoff; exact where no step
+                             is clamped -- the count is printed)
+  f64:*                      the fp64 kernel (fp64 states and adjoint: the fp64 model's gradient)
 Usage: DDR_MC_LIB=... python tools/grad_depth.py [T] [cache.npz]"""
 import sys
 import time
@@ -53,4 +57,19 @@ for k, t in (("n", n), ("q_spatial", q), ("p_spatial", p)):
     a = t.grad.cpu().numpy().astype(np.float64)
     b = ref[k]
     out[k] = float(np.linalg.norm(a - b) / np.linalg.norm(b))
-print({k: f"{v:.3g}" for k, v in out.items()}, flush=True)
+xk = runoff.detach().cpu().numpy().astype(np.float64).T.copy()  # (T, N) = clamp(x) of the kernel
+out["clamped"] = int((xk <= O.Bounds().discharge).sum())
+bo = O.route_backward(O.Network.from_coo(ns, rs, cs), r, qp, xk, W, O.Bounds())
+for k, t in (("n", n), ("q_spatial", q), ("p_spatial", p)):
+    a = t.grad.cpu().numpy().astype(np.float64)
+    out["own:" + k] = float(np.linalg.norm(a - bo[k]) / np.linalg.norm(bo[k]))
+td = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)  # noqa: E731
+n64, q64, p64 = (td(v).requires_grad_(True) for v in (r.n, r.q, r.p))
+g64 = RiverGraph(ns, rs, cs, steps_hint=T, max_block_reaches=1024)
+ro64, _, _, _ = route(g64, td(qp), n64, q64, p64, td(r.length), td(r.slope), td(r.x), consts=RouteConsts())
+ro64.backward(td(W))
+for k, t, t64 in (("n", n, n64), ("q_spatial", q, q64), ("p_spatial", p, p64)):
+    a = t.grad.cpu().numpy().astype(np.float64)
+    b = t64.grad.cpu().numpy()
+    out["f64:" + k] = float(np.linalg.norm(a - b) / np.linalg.norm(b))
+print({k: (f"{v:.3g}" if isinstance(v, float) else v) for k, v in out.items()}, flush=True)
