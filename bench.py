@@ -149,6 +149,35 @@ class FusedNet:
         return denorm(un[:, 0].contiguous(), un[:, 1].contiguous(), un[:, 2].contiguous())
 
 
+class TorchTail:
+    """clip_grad_norm_(max_norm=1) + fused Adam in PyTorch ops (the step tail of --tail torch)."""
+
+    def __init__(self, params):
+        self.params = list(params)
+        self.opt = torch.optim.Adam(self.params, lr=1e-3, fused=True)  # one launch per step, not per tensor
+
+    def zero_grad(self, set_to_none=True):
+        self.opt.zero_grad(set_to_none=set_to_none)
+
+    def step(self):
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=1.0, foreach=True)
+        self.opt.step()
+
+
+def make_tail(args, model):
+    """(optimizer, loss_fn) of the C3 step: loss_fn(daily, obs, warmup_days, inv_count) is the mean absolute
+    error over gauges x days after the warm-up (train.py:91-94); the optimizer clips to norm 1 and steps Adam."""
+    if args.tail == "fused" and args.pnet == "fused":
+        from ddr_amd.train import ClipAdam, daily_l1_loss
+
+        return ClipAdam(model.net.flat, lr=1e-3, max_norm=1.0), daily_l1_loss
+
+    def torch_l1(daily, obs, wd, inv_count):
+        return torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") * inv_count
+
+    return TorchTail(model.parameters()), torch_l1
+
+
 def denorm(un, uq, up):
     """utils.py:166-185 (torch, autograd reaches the unit-interval parameters)."""
     n = un * (RANGES["n"][1] - RANGES["n"][0]) + RANGES["n"][0]
@@ -371,6 +400,9 @@ def main():
                          "thread on its own stream) or on host threads (ddr_graph_build + upload)")
     ap.add_argument("--pnet", default="fused", choices=["fused", "torch"],
                     help="C3 parameter network: fused HIP kernels (ddr_amd.pnet) or the same network in PyTorch ops")
+    ap.add_argument("--tail", default="fused", choices=["fused", "torch"],
+                    help="C3 step tail (with --pnet fused): the daily L1 objective and clip + Adam as two HIP launches "
+                         "(ddr_amd.train) or PyTorch's l1_loss / clip_grad_norm_ / fused Adam")
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
     ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
@@ -472,7 +504,7 @@ def main():
 
         feats = tt(synthetic.reach_features(net.n, seed=11))
         model = FusedNet(args.pnet, dev)
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)  # one launch per step, not per tensor
+        opt, loss_fn = make_tail(args, model)
         # one gauge per subnetwork outlet; observations indexed by the gauge's global number
         outlets_global = np.flatnonzero(net.down < 0)
         outlets = np.flatnonzero(np.isin(ids, outlets_global))
@@ -489,11 +521,10 @@ def main():
             daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
                                    math=args.math, steps=T, qprime_hours=qp_hours)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
-            loss = torch.nn.functional.l1_loss(daily[:, wd:], obs[:, wd:], reduction="sum") / (G_global * (window.D - wd))
+            loss = loss_fn(daily, obs, wd, 1.0 / (G_global * (window.D - wd)))
             loss.backward()
             allreduce_gradients(list(model.parameters()))  # RCCL, one flat bucket
-            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0, foreach=True)
-            opt.step()
+            opt.step()  # clip_grad_norm_(max_norm=1) + Adam (train.py:99-100)
 
     else:
         from ddr_amd.geometry.statistics import geometry_statistics_from_inflow
@@ -610,6 +641,8 @@ def main():
                        "parameter_network": ({"fused": "fused HIP MLP 10-128-128-128-3 (ddr_amd.pnet, fp32 MFMA)",
                                               "torch": "PyTorch MLP 10-128-128-128-3"}[args.pnet]
                                              if args.workload == "c3" else None),
+                       "step_tail": (("fused HIP daily L1 + clip/Adam (ddr_amd.train)" if args.tail == "fused" and args.pnet == "fused"
+                                      else "PyTorch l1_loss + clip_grad_norm_ + fused Adam") if args.workload == "c3" else None),
                        "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",
                                         "faithful": "faithful (reference op order, IEEE division, fp32 faithful-class pow)",
                                         "fast": "fast (hardware rcp/log/exp fp32)"}[args.math],
@@ -686,7 +719,7 @@ def time_training_stream(args, dev):
     log(f"[stream] {M} batches resident in {time.perf_counter() - t_gen:.1f}s "
         f"({min(d['net'].n for d in data)}..{max(d['net'].n for d in data)} reaches)")
     model = FusedNet(args.pnet, dev)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    opt, loss_fn = make_tail(args, model)
     wd = args.warmup_days
     consts = RouteConsts()
     torch.cuda.synchronize()
@@ -721,10 +754,9 @@ def time_training_stream(args, dev):
         n, q, p = model(d["feats"])
         daily, _, _, _ = route(g, d["qprime"], n, q, p, d["length"], d["slope"], d["xs"], gauges=d["gz"],
                                daily=window, consts=consts, steps=T, qprime_hours=24, math=args.math)
-        loss = torch.nn.functional.l1_loss(daily[:, wd:], d["obs"][:, wd:])
+        loss = loss_fn(daily, d["obs"], wd, 1.0 / (daily.shape[0] * (window.D - wd)))
         loss.backward()
         allreduce_gradients(list(model.parameters()))
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0, foreach=True)
         opt.step()
         e1.record()
         if k >= warm:

@@ -511,6 +511,24 @@ ddr_status pnet_backward_impl(int64_t n_rows, int32_t n_features, const float* x
   return DDR_OK;
 }
 
+ddr_status daily_l1_impl(int64_t n_gauges, int64_t n_days, int64_t warmup, const float* daily, const float* obs,
+                         float inv_count, float* loss, float* grad, void* stream) {
+  if (n_gauges < 0 || n_days < 0 || warmup < 0) return fail(DDR_ERR_ARG, "daily_l1: negative size");
+  if (!loss || (n_gauges * n_days > 0 && (!daily || !obs))) return fail(DDR_ERR_ARG, "daily_l1: null argument");
+  DDR_HIP(launch_daily_l1(n_gauges, n_days, warmup, daily, obs, inv_count, loss, grad, static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+ddr_status clip_adam_impl(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
+                          float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
+                          void* stream) {
+  if (n < 0) return fail(DDR_ERR_ARG, "clip_adam: negative size");
+  if (n > 0 && (!params || !grad || !m || !v)) return fail(DDR_ERR_ARG, "clip_adam: null argument");
+  if (!(bc1 > 0.0f) || !(bc2_sqrt > 0.0f)) return fail(DDR_ERR_ARG, "clip_adam: bias corrections must be > 0");
+  DDR_HIP(launch_clip_adam(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out,
+                           static_cast<hipStream_t>(stream)));
+  return DDR_OK;
+}
+
 template <typename R>
 ddr_status state_impl(const ddr_graph* gh, const R* x_save, int64_t T, int64_t t, double qlb, int32_t flags, R* out,
                       void* stream) {
@@ -1017,6 +1035,15 @@ ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float
                                  const float* grad_q, const float* grad_p, float* grad_params, void* work,
                                  void* stream) {
   DDR_GUARD({ return pnet_backward_impl(n_rows, n_features, x, params, denorm, z_save, u_save, grad_n, grad_q, grad_p, grad_params, work, stream); })
+}
+ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, const float* daily, const float* obs,
+                            float inv_count, float* loss, float* grad, void* stream) {
+  DDR_GUARD({ return daily_l1_impl(n_gauges, n_days, warmup, daily, obs, inv_count, loss, grad, stream); })
+}
+ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
+                             float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
+                             void* stream) {
+  DDR_GUARD({ return clip_adam_impl(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, stream); })
 }
 ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
                          int32_t flags, float* out, void* stream) {

@@ -361,6 +361,22 @@ ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float
                                  const float* grad_q, const float* grad_p, float* grad_params, void* work,
                                  void* stream);
 
+/* The tail of a training step (scripts/train.py:91-100), one launch each, device pointers on `stream`:
+ * ddr_daily_l1_f32: loss[0] = inv_count * sum_{g, d >= warmup} |daily[g, d] - obs[g, d]| over (G, D) row-major
+ *   series, and (grad != NULL) grad[g, d] = inv_count * sign(daily - obs), 0 for d < warmup -- l1_loss
+ *   (train.py:91-94; inv_count = 1 / (G (D - warmup)) is its mean) and its backward in one pass.
+ * ddr_clip_adam_f32: clip_grad_norm_(max_norm) (train.py:99; max_norm <= 0: none) then one Adam step
+ *   (torch.optim.Adam, no weight decay / amsgrad; train.py:100) on a flat parameter vector of n values with
+ *   its moments m, v; bc1 = 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step) of the step being taken.
+ *   norm_out (or NULL) receives the gradient's norm before clipping.  grad is not modified.
+ * Both deterministic (one workgroup, fixed reduction order).
+ * Replaces: the ~15 PyTorch launches of l1_loss + backward, clip_grad_norm_ and Adam.step per step. */
+ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, const float* daily, const float* obs,
+                            float inv_count, float* loss, float* grad, void* stream);
+ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
+                             float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
+                             void* stream);
+
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
                                 const ddr_gauges* gauges, double discharge_lb, int32_t flags,

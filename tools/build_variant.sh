@@ -9,10 +9,10 @@ mkdir -p $OBJ
 cd $R/ddr_amd/csrc
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function $*"
 rm -f $OBJ/*.o
-for s in graph.cpp collate.cpp capi.cpp route.hip trisolve.hip geometry.hip devgraph.hip pnet.hip; do
+for s in graph.cpp collate.cpp capi.cpp route.hip trisolve.hip geometry.hip devgraph.hip pnet.hip train.hip; do
   /opt/rocm/bin/hipcc $FL -x hip -c $s -o $OBJ/$s.o &
 done
 wait
-for s in graph.cpp collate.cpp capi.cpp route.hip trisolve.hip geometry.hip devgraph.hip pnet.hip; do [ -f $OBJ/$s.o ] || { echo "variant build failed: $s"; exit 1; }; done
+for s in graph.cpp collate.cpp capi.cpp route.hip trisolve.hip geometry.hip devgraph.hip pnet.hip train.hip; do [ -f $OBJ/$s.o ] || { echo "variant build failed: $s"; exit 1; }; done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $R/ddr_amd/lib/libddr_mc_$NAME.so $OBJ/*.o
 echo built $R/ddr_amd/lib/libddr_mc_$NAME.so
