@@ -3,6 +3,8 @@
 import re
 from pathlib import Path
 
+import pytest
+
 from ddr_amd import _lib
 
 HEADER = Path(__file__).resolve().parents[1] / "include" / "ddr_mc.h"
@@ -48,3 +50,15 @@ def test_pnet_param_count_matches_python():
     for F in (1, 7, 10, 12):
         assert int(lib.ddr_pnet_param_count(F)) == param_count(F)
     assert int(lib.ddr_pnet_param_count(13)) == -1
+
+
+def test_training_tail_refuses_host_tensors():
+    """ddr_amd.train runs on the HIP device only: host tensors raise before any library call."""
+    import torch
+
+    from ddr_amd.train import ClipAdam, daily_l1_loss
+
+    with pytest.raises(RuntimeError):
+        daily_l1_loss(torch.zeros(2, 3), torch.zeros(2, 3), 0)
+    with pytest.raises(ValueError):
+        ClipAdam(torch.zeros(8))

@@ -56,6 +56,26 @@ def test_dmc_matches_reference_golden(cuda):
     assert len(list(model.parameters())) == 0
 
 
+def test_dmc_exact_adjoint_config(cuda):
+    """cfg.params.exact_adjoint: the drop-in's backward runs the exact adjoint of the fp32 trajectory (DESIGN.md
+    section 5); on the reference's own golden tree the gradients stay within the same 5e-5 of its fp32 autograd
+    and the forward is unchanged (bitwise)."""
+    case, d = golden_case("tree300", PARAMS_DEFAULT)
+    outs, grads = [], []
+    for exact in (False, True):
+        model = dmc(cfg_of({**PARAMS_DEFAULT, "exact_adjoint": exact}), device=cuda)
+        assert model.routing_engine._exact_adjoint is exact
+        sp_params = {k: torch.from_numpy(v).to(cuda).requires_grad_(True) for k, v in case.u.items()}
+        out = model(routing_dataclass=golden_dataclass(case), streamflow=torch.from_numpy(case.qprime),
+                    spatial_parameters=sp_params)["runoff"]
+        (out * torch.from_numpy(case.W).to(cuda)).sum().backward()
+        outs.append(out.detach().cpu().numpy())
+        grads.append({k: v.grad.cpu().numpy() for k, v in sp_params.items()})
+    np.testing.assert_array_equal(outs[0], outs[1])
+    for k in grads[1]:
+        assert normrel(grads[1][k], d[f"ref_grad_{k}"]) <= 5e-5, k
+
+
 def test_dmc_gauge_mode_sandbox_default_p(cuda):
     case, d = golden_case("sandbox", PARAMS_MOCK)
     model = dmc(cfg_of(PARAMS_MOCK), device=cuda)
