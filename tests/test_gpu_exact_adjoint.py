@@ -102,3 +102,47 @@ def test_exact_adjoint_state_gradients(cuda, blk, mode):
                       gkw={"max_block_reaches": 64, "target_blocks": 1 << 20})
         for k in keys:
             np.testing.assert_array_equal(cut[k], ex[k], err_msg=k)
+
+
+def test_exact_adjoint_gauge_daily_store(cuda):
+    """Gauge mode over a daily q' store with flow_scale and a missing divide (the C3 training layout: the qc
+    re-read goes through the store's row layout), against the fp64 oracle adjoint on the oracle's fp32
+    states (the kernel's, bit for bit: exact forward math)."""
+    from ddr_amd.ops import GaugeMap
+
+    net = synthetic.hack_basin(30000, seed=23, single_inflow=0.3)
+    T, hours = 72, 24
+    at = synthetic.reach_attributes(net.n, 23)
+    r = _reaches(synthetic.unit_parameters(net.n, 23), at)
+    rng = np.random.default_rng(23)
+    qstore = synthetic.lateral_inflow(net.n, T // hours, 24)
+    fs = rng.uniform(0.5, 1.5, net.n).astype(np.float32)
+    valid = np.ones(net.n, np.uint8)
+    valid[7] = 0
+    outflow = [np.array([net.n - 1]), np.array([100, 200, 300]), np.array([5000])]
+    tt = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)  # noqa: E731
+    n, q, p = (tt(v).requires_grad_(True) for v in (r.n, r.q, r.p))
+    qp = tt(qstore).requires_grad_(True)
+    g = RiverGraph(net.n, net.rows, net.cols, steps_hint=T)
+    gz = GaugeMap.build(outflow, net.n, cuda)
+    runoff, _, _, _ = route(g, qp, n, q, p, tt(r.length), tt(r.slope), tt(r.x), flow_scale=tt(fs), gauges=gz,
+                            consts=RouteConsts(), steps=T, qprime_hours=hours, qprime_valid=torch.from_numpy(valid),
+                            exact_adjoint=True)
+    W = rng.uniform(0, 1, tuple(runoff.shape)).astype(np.float32)
+    runoff.backward(tt(W))
+    # the oracle on the hourly, scaled, filled series the kernel routes (fp32, as the kernel's gather forms it)
+    qh = np.repeat(qstore, hours, axis=0)[:T].copy()
+    qh[:, valid == 0] = np.float32(0.001)
+    qh = (qh * fs[None, :]).astype(np.float32)
+    netO = O.Network.from_coo(net.n, net.rows, net.cols)
+    fw = O.route(netO, r, qh, O.Bounds(), dtype=np.float32, outflow_idx=outflow)
+    bw = O.route_backward(netO, r, qh, fw["x"], W, O.Bounds(), outflow_idx=outflow, want_qprime=True)
+    gh = bw["qprime"] * fs[None, :].astype(np.float64)
+    gh[:, valid == 0] = 0.0
+    gstore = np.zeros(qstore.shape)
+    for t in range(T):
+        gstore[t // hours] += gh[t]
+    res = {"n": n.grad, "q_spatial": q.grad, "p_spatial": p.grad}
+    for k, v in res.items():
+        assert normrel(v.cpu().numpy(), bw[k]) <= BAR, k
+    assert normrel(qp.grad.cpu().numpy(), gstore) <= BAR
