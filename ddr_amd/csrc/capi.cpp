@@ -11,6 +11,7 @@
 
 #include "internal.h"
 #include "route_args.h"
+#include "train.h"
 
 namespace ddr {
 
@@ -520,11 +521,12 @@ ddr_status daily_l1_impl(int64_t n_gauges, int64_t n_days, int64_t warmup, const
 }
 ddr_status clip_adam_impl(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
                           float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                          void* stream) {
+                          void* work, void* stream) {
   if (n < 0) return fail(DDR_ERR_ARG, "clip_adam: negative size");
   if (n > 0 && (!params || !grad || !m || !v)) return fail(DDR_ERR_ARG, "clip_adam: null argument");
   if (!(bc1 > 0.0f) || !(bc2_sqrt > 0.0f)) return fail(DDR_ERR_ARG, "clip_adam: bias corrections must be > 0");
-  DDR_HIP(launch_clip_adam(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out,
+  if (!work) return fail(DDR_ERR_ARG, "clip_adam: null workspace (ddr_clip_adam_work_bytes)");
+  DDR_HIP(launch_clip_adam(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, work,
                            static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -1040,10 +1042,11 @@ ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, co
                             float inv_count, float* loss, float* grad, void* stream) {
   DDR_GUARD({ return daily_l1_impl(n_gauges, n_days, warmup, daily, obs, inv_count, loss, grad, stream); })
 }
+int64_t ddr_clip_adam_work_bytes(void) { return (int64_t)clip_adam_work_bytes(); }
 ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
                              float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                             void* stream) {
-  DDR_GUARD({ return clip_adam_impl(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, stream); })
+                             void* work, void* stream) {
+  DDR_GUARD({ return clip_adam_impl(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, work, stream); })
 }
 ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
                          int32_t flags, float* out, void* stream) {

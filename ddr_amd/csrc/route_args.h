@@ -152,12 +152,6 @@ hipError_t launch_pnet_forward(int64_t N, int F, const float* X, const float* P,
                                float* const out[3], hipStream_t stream);
 hipError_t launch_pnet_backward(int64_t N, int F, const float* X, const float* P, const float* denorm, const float* Z,
                                 const float* U, const float* const gout[3], float* grad, void* work, hipStream_t stream);
-// The C3 step's tail (train.hip): daily L1 objective + its gradient; gradient clipping + Adam
-hipError_t launch_daily_l1(int64_t G, int64_t D, int64_t wd, const float* daily, const float* obs, float inv_count,
-                           float* loss, float* grad, hipStream_t stream);
-hipError_t launch_clip_adam(int64_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
-                            float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                            hipStream_t stream);
 // geometry.hip: windows of up to kGeoLongMaxDays days (~89 years; beyond 512 days one workgroup per
 // reach sorts each variable in LDS)
 constexpr int64_t kGeoLongMaxDays = 32768;

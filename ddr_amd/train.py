@@ -1,4 +1,4 @@
-"""The tail of the C3 training step on the device in two launches (``csrc/train.hip``).
+"""The tail of the C3 training step on the device in three launches (``csrc/train.hip``).
 
 The reference's loop (``scripts/train.py:91-100``) ends each mini-batch with ``l1_loss`` over the gauges'
 daily series after the warm-up, ``loss.backward()``, ``clip_grad_norm_(max_norm=1.0)`` and ``optimizer.step()``
@@ -10,7 +10,7 @@ backward; the norm, the clip factor, the scaling; Adam's moment updates).  Here:
 * :class:`ClipAdam` -- clip + Adam over one flat parameter vector (``ddr_clip_adam_f32``), e.g.
   :class:`ddr_amd.pnet.ParamNet`'s ``flat``.
 
-Both are deterministic (one workgroup, fixed reduction order) and run on the HIP device only.
+Both are deterministic (fixed slices and reduction order) and run on the HIP device only.
 """
 
 from __future__ import annotations
@@ -60,7 +60,7 @@ def daily_l1_loss(daily: torch.Tensor, obs: torch.Tensor, warmup: int, inv_count
 
 class ClipAdam:
     """``clip_grad_norm_(max_norm)`` then ``torch.optim.Adam(lr, betas, eps)`` (no weight decay) on one flat
-    fp32 parameter tensor, in one launch per step.  ``max_norm`` <= 0 disables clipping.  ``last_norm`` holds the
+    fp32 parameter tensor, in two launches per step (64 workgroups).  ``max_norm`` <= 0 disables clipping.  ``last_norm`` holds the
     gradient norm of the last step (a device scalar, clip_grad_norm_'s return value)."""
 
     def __init__(self, param: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
@@ -72,6 +72,7 @@ class ClipAdam:
         self.m = torch.zeros_like(param)
         self.v = torch.zeros_like(param)
         self.last_norm = torch.zeros((), device=param.device, dtype=torch.float32)
+        self.work = torch.empty(int(_lib.load().ddr_clip_adam_work_bytes()), device=param.device, dtype=torch.uint8)
         self.steps = 0
 
     def zero_grad(self, set_to_none: bool = True) -> None:
@@ -94,4 +95,4 @@ class ClipAdam:
                                                  self.m.data_ptr(), self.v.data_ptr(), C.c_float(self.lr), C.c_float(b1),
                                                  C.c_float(b2), C.c_float(self.eps), C.c_float(bc1), C.c_float(bc2s),
                                                  C.c_float(self.max_norm), self.last_norm.data_ptr(),
-                                                 _lib.stream_ptr(self.param.device)))
+                                                 self.work.data_ptr(), _lib.stream_ptr(self.param.device)))

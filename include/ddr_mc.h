@@ -368,14 +368,16 @@ ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float
  * ddr_clip_adam_f32: clip_grad_norm_(max_norm) (train.py:99; max_norm <= 0: none) then one Adam step
  *   (torch.optim.Adam, no weight decay / amsgrad; train.py:100) on a flat parameter vector of n values with
  *   its moments m, v; bc1 = 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step) of the step being taken.
- *   norm_out (or NULL) receives the gradient's norm before clipping.  grad is not modified.
- * Both deterministic (one workgroup, fixed reduction order).
+ *   norm_out (or NULL) receives the gradient's norm before clipping.  grad is not modified.  work: device
+ *   scratch of ddr_clip_adam_work_bytes() bytes.
+ * Both deterministic (fixed slices and reduction order).
  * Replaces: the ~15 PyTorch launches of l1_loss + backward, clip_grad_norm_ and Adam.step per step. */
 ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, const float* daily, const float* obs,
                             float inv_count, float* loss, float* grad, void* stream);
+int64_t ddr_clip_adam_work_bytes(void);
 ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
                              float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                             void* stream);
+                             void* work, void* stream);
 
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
