@@ -403,6 +403,9 @@ def main():
     ap.add_argument("--tail", default="fused", choices=["fused", "torch"],
                     help="C3 step tail (with --pnet fused): the daily L1 objective and clip + Adam as two HIP launches "
                          "(ddr_amd.train) or PyTorch's l1_loss / clip_grad_norm_ / fused Adam")
+    ap.add_argument("--graph", action="store_true",
+                    help="C3, no process group: capture the whole training step into one HIP graph (ddr_amd.capture) "
+                         "and time its replays; kernel times come from eager steps before the capture")
     ap.add_argument("--fast-math", action="store_true",
                     help="forward coefficients in hardware-approximate fp32 math (route(math='fast'))")
     ap.add_argument("--math", default=None, choices=["exact", "faithful", "fast"],
@@ -547,6 +550,8 @@ def main():
         step()
         e1.record()
         ev.append((e0, e1))
+        if graph_mode:
+            return
         for w_, key in ((0, "forward"), (1, "backward")):
             if key == "backward" and not spec["grad"]:
                 continue
@@ -560,6 +565,19 @@ def main():
         step()
     _lib.check(lib.ddr_set_kernel_timing(1))
     torch.cuda.synchronize()
+    graph_mode = None
+    if args.graph:
+        if args.workload != "c3" or dist is not None or args.tail != "fused" or args.pnet != "fused":
+            raise SystemExit("--graph: the C3 step with the fused network and tail, without a process group")
+        from ddr_amd.capture import CapturedStep
+
+        # the routing kernels' times from eager steps (the library's timers are off inside a capture)
+        for _ in range(2):
+            timed_step()
+        ev.clear()
+        step = CapturedStep(step, warmup=1, device=dev)
+        graph_mode = "whole step captured into one HIP graph (ddr_amd.capture); kernel ms from 2 eager steps"
+        torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -641,6 +659,7 @@ def main():
                        "parameter_network": ({"fused": "fused HIP MLP 10-128-128-128-3 (ddr_amd.pnet, fp32 MFMA)",
                                               "torch": "PyTorch MLP 10-128-128-128-3"}[args.pnet]
                                              if args.workload == "c3" else None),
+                       "step_graph": graph_mode,
                        "step_tail": (("fused HIP daily L1 + clip/Adam (ddr_amd.train)" if args.tail == "fused" and args.pnet == "fused"
                                       else "PyTorch l1_loss + clip_grad_norm_ + fused Adam") if args.workload == "c3" else None),
                        "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",

@@ -123,8 +123,8 @@ _SIGS = {
     "ddr_pnet_backward_f32": (C.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "ddr_daily_l1_f32": (C.c_int, [_I64, _I64, _I64, _P, _P, C.c_float, _P, _P, _P]),
     "ddr_clip_adam_work_bytes": (_I64, []),
-    "ddr_clip_adam_f32": (C.c_int, [_I64, _P, _P, _P, _P, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
-                                    C.c_float, C.c_float, _P, _P, _P]),
+    "ddr_clip_adam_f32": (C.c_int, [_I64, _P, _P, _P, _P, C.c_float, C.c_float, C.c_float, C.c_float, _P,
+                                    C.c_float, _P, _P, _P]),
     "ddr_state_f32": (C.c_int, [_P, _P, _I64, _I64, C.c_double, _I32, _P, _P]),
     "ddr_state_f64": (C.c_int, [_P, _P, _I64, _I64, C.c_double, _I32, _P, _P]),
     "ddr_gauge_reduce_f32": (C.c_int, [_P, _P, _I64, C.POINTER(Gauges), C.c_double, _I32, _P, _P]),

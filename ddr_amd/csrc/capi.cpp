@@ -178,8 +178,19 @@ hipError_t nan_check_mark(const void* status, hipStream_t s) {
   return hipEventRecord(c.ev, s);
 }
 
+// Stream capture (a hipGraph of a whole training step, e.g. torch.cuda.graph): the launches are recorded and
+// replayed later, so the host-side bookkeeping of a launch -- the status harvest (a D2H copy and an event per
+// launch, polled by later calls), the kernel timers, the wait for the graph's upload event (recorded outside
+// the capture: capture a step only after the graph has been used once) -- is skipped while the stream
+// captures.  A timed-out hand-off inside a replayed step still writes NaN into its outputs.
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+hipError_t ready_for(const Graph* g, hipStream_t s) { return capturing(s) ? hipSuccess : graph_ready(g, s); }
+
 hipError_t timing_mark(int which, int edge, hipStream_t s) {
-  if (!g_timing.on) return hipSuccess;
+  if (!g_timing.on || capturing(s)) return hipSuccess;
   hipEvent_t& e = g_timing.ev[which][edge];
   if (!e) {
     hipError_t r = hipEventCreate(&e);
@@ -306,10 +317,13 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   // (a hot start, the daily accumulation) would leave the epochs of all later launches off by one
   if (g->split.nranks > 0 && (T < 2 || (flags & DDR_FWD_ACCUMULATE)))
     return fail(DDR_ERR_ARG, "split basin: hot-start (T = 1) and accumulation launches are not supported");
-  if ((st = g_pending.check(false))) return st;
-  if ((st = check_launchable<R>(g, false))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DDR_HIP(graph_ready(g, s));
+  const bool cap = capturing(s);
+  if (cap && (g->split.nranks > 0 || (flags & DDR_FWD_CHECK_QPRIME)))
+    return fail(DDR_ERR_ARG, "stream capture: split-basin launches and the q' NaN check cannot be captured");
+  if (!cap && (st = g_pending.check(false))) return st;
+  if ((st = check_launchable<R>(g, false))) return st;
+  DDR_HIP(ready_for(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bnd, 0xFF, sizeof(double) * g->n_cut * T, s));
   RouteArgs a;
@@ -332,7 +346,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
   DDR_HIP(timing_mark(0, 1, s));
   DDR_HIP(launch_split_finish<R>(g, a, s));
   // runoff (N, T) is written by the routing kernel itself (16-B row segments every 4 steps)
-  return g_pending.enqueue(status, s, "forward", gh);
+  return cap ? DDR_OK : g_pending.enqueue(status, s, "forward", gh);
 }
 
 template <typename R>
@@ -370,10 +384,12 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
     if (gqp && qp_rows < (T + std::max<int64_t>(1, r->qprime_hours) - 1) / std::max<int64_t>(1, r->qprime_hours))
       return fail(DDR_ERR_ARG, "grad_qprime has fewer rows than the window reads");
   }
-  if ((st = g_pending.check(false))) return st;
-  if ((st = check_launchable<R>(g, true))) return st;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DDR_HIP(graph_ready(g, s));
+  const bool cap = capturing(s);
+  if (cap && g->split.nranks > 0) return fail(DDR_ERR_ARG, "stream capture: split-basin launches cannot be captured");
+  if (!cap && (st = g_pending.check(false))) return st;
+  if ((st = check_launchable<R>(g, true))) return st;
+  DDR_HIP(ready_for(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
   DDR_HIP(hipMemsetAsync(bwd_bnd + 2 * g->n_cut * T, 0, sizeof(double) * 3 * g->n, s));
@@ -410,7 +426,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   DDR_HIP(launch_route<R>(g, a, true, s));
   DDR_HIP(timing_mark(1, 1, s));
   if (gqp) DDR_HIP(launch_scatter_qprime_grad<R>(g, a, qp_rows, gqp, s));
-  return g_pending.enqueue(status, s, "backward", gh);
+  return cap ? DDR_OK : g_pending.enqueue(status, s, "backward", gh);
 }
 
 template <typename R>
@@ -442,7 +458,7 @@ ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   ddr_status st = gauge_args<R>(gh, x_save, T, gz, qlb, flags, a);
   if (st) return st;
   if (!out) return fail(DDR_ERR_ARG, "null gauge output");
-  DDR_HIP(graph_ready(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
+  DDR_HIP(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge<R>(a, x_save, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -461,7 +477,7 @@ ddr_status gauge_daily_impl(const ddr_graph* gh, const R* x_save, int64_t T, con
   if (st) return st;
   if ((st = check_window(T, t0, L, D))) return st;
   if (!out) return fail(DDR_ERR_ARG, "null daily output");
-  DDR_HIP(graph_ready(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
+  DDR_HIP(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge_daily<R>(a, x_save, t0, L, D, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -520,13 +536,13 @@ ddr_status daily_l1_impl(int64_t n_gauges, int64_t n_days, int64_t warmup, const
   return DDR_OK;
 }
 ddr_status clip_adam_impl(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
-                          float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                          void* work, void* stream) {
+                          float beta2, float eps, float* step, float max_norm, float* norm_out, void* work,
+                          void* stream) {
   if (n < 0) return fail(DDR_ERR_ARG, "clip_adam: negative size");
   if (n > 0 && (!params || !grad || !m || !v)) return fail(DDR_ERR_ARG, "clip_adam: null argument");
-  if (!(bc1 > 0.0f) || !(bc2_sqrt > 0.0f)) return fail(DDR_ERR_ARG, "clip_adam: bias corrections must be > 0");
-  if (!work) return fail(DDR_ERR_ARG, "clip_adam: null workspace (ddr_clip_adam_work_bytes)");
-  DDR_HIP(launch_clip_adam(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, work,
+  if (!(beta1 >= 0.0f && beta1 < 1.0f) || !(beta2 >= 0.0f && beta2 < 1.0f)) return fail(DDR_ERR_ARG, "clip_adam: betas in [0, 1)");
+  if (!step || !work) return fail(DDR_ERR_ARG, "clip_adam: null step counter or workspace (ddr_clip_adam_work_bytes)");
+  DDR_HIP(launch_clip_adam(n, params, grad, m, v, lr, beta1, beta2, eps, step, max_norm, norm_out, work,
                            static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -541,7 +557,7 @@ ddr_status state_impl(const ddr_graph* gh, const R* x_save, int64_t T, int64_t t
   // a split rank holds the states of its own blocks only
   if (g->split.nranks > 0) return fail(DDR_ERR_ARG, "split basin: the saved states are per rank");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DDR_HIP(graph_ready(g, s));
+  DDR_HIP(ready_for(g, s));
   DDR_HIP(launch_state_at<R>(g, T, t, qlb, (flags & DDR_FWD_CARRY) != 0, x_save, out, s));
   return DDR_OK;
 }
@@ -1044,9 +1060,9 @@ ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, co
 }
 int64_t ddr_clip_adam_work_bytes(void) { return (int64_t)clip_adam_work_bytes(); }
 ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
-                             float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                             void* work, void* stream) {
-  DDR_GUARD({ return clip_adam_impl(n, params, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, work, stream); })
+                             float beta2, float eps, float* step, float max_norm, float* norm_out, void* work,
+                             void* stream) {
+  DDR_GUARD({ return clip_adam_impl(n, params, grad, m, v, lr, beta1, beta2, eps, step, max_norm, norm_out, work, stream); })
 }
 ddr_status ddr_state_f32(const ddr_graph* g, const float* x_save, int64_t T, int64_t t, double discharge_lb,
                          int32_t flags, float* out, void* stream) {

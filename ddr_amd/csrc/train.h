@@ -12,6 +12,6 @@ hipError_t launch_daily_l1(int64_t G, int64_t D, int64_t wd, const float* daily,
 // device scratch of launch_clip_adam (per-workgroup partial sums of squares)
 size_t clip_adam_work_bytes();
 hipError_t launch_clip_adam(int64_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
-                            float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                            void* work, hipStream_t stream);
+                            float beta2, float eps, float* step, float max_norm, float* norm_out, void* work,
+                            hipStream_t stream);
 }  // namespace ddr

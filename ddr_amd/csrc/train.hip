@@ -59,8 +59,7 @@ struct AdamArgs {
   float* m;
   float* v;
   float lr, beta1, beta2, eps;
-  float bc1;        // 1 - beta1^step
-  float bc2_sqrt;   // sqrt(1 - beta2^step)
+  float* step;      // device step counter (fp32, like torch's capturable Adam): incremented by this update
   float max_norm;   // <= 0: no clipping
   float* norm_out;  // the gradient's total norm before clipping (clip_grad_norm_'s return value), or null
   double* partial;  // [kAdamWgs] per-workgroup sums of squares
@@ -92,11 +91,16 @@ __global__ void __launch_bounds__(kAdamThreads) adam_norm_kernel(AdamArgs a) {
   }
   const double s = block_sum256(ss, red);
   if (threadIdx.x == 0) a.partial[blockIdx.x] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.step[0] = a.step[0] + 1.0f;  // read by adam_step_kernel, next launch
 }
 
 __global__ void __launch_bounds__(kAdamThreads) adam_step_kernel(AdamArgs a) {
-  __shared__ float coef_s;
+  __shared__ float coef_s, step_s, bc2s_s;
   if (threadIdx.x == 0) {
+    // bias corrections of this step on the device (torch's capturable Adam: fp32 step tensor)
+    const float t = a.step[0];
+    step_s = a.lr / (1.0f - powf(a.beta1, t));
+    bc2s_s = sqrtf(1.0f - powf(a.beta2, t));
     double s = 0.0;
     for (int w = 0; w < kAdamWgs; ++w) s += a.partial[w];
     const float norm = (float)sqrt(s);
@@ -105,16 +109,15 @@ __global__ void __launch_bounds__(kAdamThreads) adam_step_kernel(AdamArgs a) {
     coef_s = a.max_norm > 0.0f ? fminf(a.max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
   }
   __syncthreads();
-  const float coef = coef_s;
+  const float coef = coef_s, step = step_s, bc2_sqrt = bc2s_s;
   const float omb1 = 1.0f - a.beta1, omb2 = 1.0f - a.beta2;
-  const float step = a.lr / a.bc1;
   for (int64_t i = (int64_t)blockIdx.x * kAdamThreads + threadIdx.x; i < a.n; i += (int64_t)kAdamWgs * kAdamThreads) {
     const float g = a.grad[i] * coef;
     const float m = fmaf(omb1, g - a.m[i], a.m[i]);           // exp_avg.lerp_(grad, 1 - beta1)
     const float v = fmaf(a.beta2, a.v[i], omb2 * g * g);      // exp_avg_sq * beta2 + (1 - beta2) g^2
     a.m[i] = m;
     a.v[i] = v;
-    const float den = sqrtf(v) / a.bc2_sqrt + a.eps;
+    const float den = sqrtf(v) / bc2_sqrt + a.eps;
     a.param[i] = a.param[i] - step * (m / den);
   }
 }
@@ -130,9 +133,9 @@ hipError_t launch_daily_l1(int64_t G, int64_t D, int64_t wd, const float* daily,
 size_t clip_adam_work_bytes() { return sizeof(double) * kAdamWgs; }
 
 hipError_t launch_clip_adam(int64_t n, float* param, const float* grad, float* m, float* v, float lr, float beta1,
-                            float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                            void* work, hipStream_t stream) {
-  AdamArgs a{n, param, grad, m, v, lr, beta1, beta2, eps, bc1, bc2_sqrt, max_norm, norm_out, static_cast<double*>(work)};
+                            float beta2, float eps, float* step, float max_norm, float* norm_out, void* work,
+                            hipStream_t stream) {
+  AdamArgs a{n, param, grad, m, v, lr, beta1, beta2, eps, step, max_norm, norm_out, static_cast<double*>(work)};
   hipLaunchKernelGGL(adam_norm_kernel, dim3(kAdamWgs), dim3(kAdamThreads), 0, stream, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -16,7 +16,6 @@ Both are deterministic (fixed slices and reduction order) and run on the HIP dev
 from __future__ import annotations
 
 import ctypes as C
-import math
 
 import torch
 
@@ -73,7 +72,8 @@ class ClipAdam:
         self.v = torch.zeros_like(param)
         self.last_norm = torch.zeros((), device=param.device, dtype=torch.float32)
         self.work = torch.empty(int(_lib.load().ddr_clip_adam_work_bytes()), device=param.device, dtype=torch.uint8)
-        self.steps = 0
+        # the step counter lives on the device (as torch's capturable Adam): a captured step replays correctly
+        self.step_count = torch.zeros((), device=param.device, dtype=torch.float32)
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         if set_to_none:
@@ -87,12 +87,9 @@ class ClipAdam:
         if g is None:
             return
         g = g.contiguous()
-        self.steps += 1
         b1, b2 = self.betas
-        bc1 = 1.0 - b1 ** self.steps
-        bc2s = math.sqrt(1.0 - b2 ** self.steps)
         _lib.check(_lib.load().ddr_clip_adam_f32(self.param.numel(), self.param.data_ptr(), g.data_ptr(),
                                                  self.m.data_ptr(), self.v.data_ptr(), C.c_float(self.lr), C.c_float(b1),
-                                                 C.c_float(b2), C.c_float(self.eps), C.c_float(bc1), C.c_float(bc2s),
+                                                 C.c_float(b2), C.c_float(self.eps), self.step_count.data_ptr(),
                                                  C.c_float(self.max_norm), self.last_norm.data_ptr(),
                                                  self.work.data_ptr(), _lib.stream_ptr(self.param.device)))

@@ -367,7 +367,9 @@ ddr_status ddr_pnet_backward_f32(int64_t n_rows, int32_t n_features, const float
  *   (train.py:91-94; inv_count = 1 / (G (D - warmup)) is its mean) and its backward in one pass.
  * ddr_clip_adam_f32: clip_grad_norm_(max_norm) (train.py:99; max_norm <= 0: none) then one Adam step
  *   (torch.optim.Adam, no weight decay / amsgrad; train.py:100) on a flat parameter vector of n values with
- *   its moments m, v; bc1 = 1 - beta1^step, bc2_sqrt = sqrt(1 - beta2^step) of the step being taken.
+ *   its moments m, v; step is a device fp32 counter (0 before the first step) that the launch increments and
+ *   takes the bias corrections from, as torch's capturable Adam does -- no host value, so the launch can be
+ *   captured into a graph and replayed.
  *   norm_out (or NULL) receives the gradient's norm before clipping.  grad is not modified.  work: device
  *   scratch of ddr_clip_adam_work_bytes() bytes.
  * Both deterministic (fixed slices and reduction order).
@@ -376,8 +378,8 @@ ddr_status ddr_daily_l1_f32(int64_t n_gauges, int64_t n_days, int64_t warmup, co
                             float inv_count, float* loss, float* grad, void* stream);
 int64_t ddr_clip_adam_work_bytes(void);
 ddr_status ddr_clip_adam_f32(int64_t n, float* params, const float* grad, float* m, float* v, float lr, float beta1,
-                             float beta2, float eps, float bc1, float bc2_sqrt, float max_norm, float* norm_out,
-                             void* work, void* stream);
+                             float beta2, float eps, float* step, float max_norm, float* norm_out, void* work,
+                             void* stream);
 
 /* Gauge reduction of a forward's saved states x_save: runoff (G, T). */
 ddr_status ddr_gauge_reduce_f32(const ddr_graph* g, const float* x_save, int64_t T,
