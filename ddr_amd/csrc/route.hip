@@ -55,6 +55,15 @@ namespace ddr {
 #ifndef DDR_BWD_EARLY_MAX_KR
 #define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
 #endif
+// The backward's steady ticks without the dL/drunoff group clamps, and the KR = 4 group select as two bit tests
+// and three selects instead of a ternary chain the compiler turned into divergent branches: C5 backward
+// 57.3 -> 53.9 ms (profiles/r05/ab_r05.txt item 10); the same loaded values, the same bits
+#ifndef DDR_BWD_GRAD_NOCLAMP
+#define DDR_BWD_GRAD_NOCLAMP 1
+#endif
+#ifndef DDR_BWD_SEL_BITS
+#define DDR_BWD_SEL_BITS 1
+#endif
 
 namespace {
 
@@ -1318,7 +1327,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   auto load_grad_out = [&](int ref, int64_t base, int gs, bool un) {
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
     const bool v4 = vec4 && !(un && (base & 3) != 0);
-    auto cl = [&](int64_t i) { return i < 0 ? int64_t(0) : (i < T ? i : T - 1); };
+    // !un (steady ticks): the group's steps lie in [1, T - 2], so the clamps (int64 compares and selects the
+    // compiler hoists above the vec4 branch, run by the whole wave every tick) are dropped
+    auto cl = [&](int64_t i) { return (!un && DDR_BWD_GRAD_NOCLAMP) ? i : (i < 0 ? int64_t(0) : (i < T ? i : T - 1)); };
     const int64_t i0 = cl(base), i1 = cl(base + 1), i2 = cl(base + 2), i3 = cl(base + 3);
     // m0: the gauge's t = 0 sum passed its clamp (state gradients only; mmc.py:398-412)
     auto add_row = [&](const R* row, bool m0) {
@@ -1338,10 +1349,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         v3 = v3 + ((m0 || base != -3) ? row[i3] : R(0));
       }
     };
+    // a row's four values as loaded: no arithmetic on them in this tick, so the wave does not wait for the load
+    // (it lands by the next tick's top; adding them to 0 would consume it now -- a full memory round trip)
+    auto raw_row = [&](const R* row) {
+      if (v4) {
+        if constexpr (sizeof(R) == 4) {
+          const float4 v = load_grad4(row + base);
+          return make_grad4(v.x, v.y, v.z, v.w);
+        } else {
+          const double2 u = reinterpret_cast<const double2*>(row + base)[0];
+          const double2 w = reinterpret_cast<const double2*>(row + base)[1];
+          return make_grad4(u.x, u.y, w.x, w.y);
+        }
+      }
+      return make_grad4(row[i0], row[i1], row[i2], row[i3]);
+    };
     if (a.g_roff) {
       const bool z = GS && a.gmask0 && base <= 0;  // the group holds step 0
       if (gs >= 0) {
         // the reach's only gauge (kGReg): the row address needs no dependent index loads in the tick
+        // (its values as loaded instead of added to 0, so that this tick does not wait for them: no change
+        // at c3s8, r05_gr)
         add_row(gout + (int64_t)gs * T, !(z && a.gmask0[gs] == 0));
         return make_grad4(v0, v1, v2, v3);
       }
@@ -1352,7 +1380,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       return make_grad4(v0, v1, v2, v3);
     }
-    // one reach row: the loaded values as they are (adding them to 0 would consume the load now)
+    // one reach row: the loaded values as they are
 #ifndef DDR_EXP_GRAD_DUMMY
 #define DDR_EXP_GRAD_DUMMY 0  // timing experiment only: dL/drunoff read from a 256-KB L2-resident window (wrong values)
 #endif
@@ -1364,18 +1392,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         return make_grad4(v.x, v.y, v.z, v.w);
       }
     }
-    const R* row = gout + (int64_t)ref * T;
-    if (v4) {
-      if constexpr (sizeof(R) == 4) {
-        const float4 v = load_grad4(row + base);
-        return make_grad4(v.x, v.y, v.z, v.w);
-      } else {
-        const double2 u = reinterpret_cast<const double2*>(row + base)[0];
-        const double2 w = reinterpret_cast<const double2*>(row + base)[1];
-        return make_grad4(u.x, u.y, w.x, w.y);
-      }
-    }
-    return make_grad4(row[i0], row[i1], row[i2], row[i3]);
+    return raw_row(gout + (int64_t)ref * T);
   };
   // ... plus the state seeds of steps T - 1 and T - 2 (a.gseed).  Only outside the steady ticks (seeded: the
   // steady range then starts late enough that no steady tick loads the groups of those steps), so the steady
@@ -1553,7 +1570,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         g1[k] = g0[k];
       } else {
         const int e4 = P.t & 3;
-        P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+        if constexpr (DDR_BWD_SEL_BITS) {
+          // two bit tests, three selects (the ternary chain on e4 compiles into divergent branches)
+          const bool b0 = (e4 & 1) != 0, b1 = (e4 & 2) != 0;
+          const R lo = b0 ? g1[k] : g0[k], hi = b0 ? g3[k] : g2[k];
+          P.gk = b1 ? hi : lo;
+        } else {
+          P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
+        }
       }
       P.xtk = xc[k];
       P.st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(P.rs);
