@@ -55,7 +55,7 @@ namespace ddr {
 #ifndef DDR_BWD_EARLY_MAX_KR
 #define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
 #endif
-// The backward's steady ticks without the dL/drunoff group clamps, and the KR = 4 group select as two bit tests
+// The KR = 4 backward's steady ticks without the dL/drunoff group clamps, and its group select as two bit tests
 // and three selects instead of a ternary chain the compiler turned into divergent branches: C5 backward
 // 57.3 -> 53.9 ms (profiles/r05/ab_r05.txt item 10); the same loaded values, the same bits
 #ifndef DDR_BWD_GRAD_NOCLAMP
@@ -1328,8 +1328,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     R v0 = R(0), v1 = R(0), v2 = R(0), v3 = R(0);
     const bool v4 = vec4 && !(un && (base & 3) != 0);
     // !un (steady ticks): the group's steps lie in [1, T - 2], so the clamps (int64 compares and selects the
-    // compiler hoists above the vec4 branch, run by the whole wave every tick) are dropped
-    auto cl = [&](int64_t i) { return (!un && DDR_BWD_GRAD_NOCLAMP) ? i : (i < 0 ? int64_t(0) : (i < T ? i : T - 1)); };
+    // compiler hoists above the vec4 branch, run by the whole wave every tick) are dropped -- at KR = 4 (at
+    // KR = 1 the light C5-shaped backward measured 6 % slower without them, r05_nc0)
+    auto cl = [&](int64_t i) {
+      return (!un && DDR_BWD_GRAD_NOCLAMP && KR >= 4) ? i : (i < 0 ? int64_t(0) : (i < T ? i : T - 1));
+    };
     const int64_t i0 = cl(base), i1 = cl(base + 1), i2 = cl(base + 2), i3 = cl(base + 3);
     // m0: the gauge's t = 0 sum passed its clamp (state gradients only; mmc.py:398-412)
     auto add_row = [&](const R* row, bool m0) {
