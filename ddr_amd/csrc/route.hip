@@ -480,7 +480,12 @@ __device__ __forceinline__ const R* qs_at(const RouteArgs& a, const BlockDesc& B
 // (DDR_FWD_FAITHFUL_MATH: exact op order and IEEE divisions, fp32 faithful-class pow).
 // XB: the x slots' buffer count when not the KR rule's (fwd_xbuf): 2 = parity-indexed slots and one barrier
 // per tick at KR = 4 too, where the launch finds the LDS for them (launch_route_kr)
-template <typename R, int KR, int MATH, int XB = 0>
+// PL (plain): the launch has none of the rarely used options -- no split basin, no profile, no daily
+// accumulation -- and 1: runoff written with 16-B rows, q' from the tick-major gather; 2: no runoff (gauge mode),
+// tick-major q'; 4: no runoff, q' from the row layout (daily q', qs_rows); so their tests and the uniform values
+// behind them (held in scalar registers, spilled at KR = 4) leave the tick loop (C5 forward -6 %, C4 -8 %,
+// C2 -15 %: profiles/r05/ab_r05.txt item 11)
+template <typename R, int KR, int MATH, int XB = 0, int PL = 0>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
 #ifndef DDR_FWD_NP
@@ -518,7 +523,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith, KR >= DDR_OPQ_INF_MIN_KR);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
-  const bool accum = a.flags & DDR_FWD_ACCUMULATE;  // every step a hot start (daily accumulation)
+  const bool accum = !PL && (a.flags & DDR_FWD_ACCUMULATE);  // every step a hot start (daily accumulation)
+  auto* const aprof = PL ? nullptr : a.prof;  // per-block tick profile (--block-profile)
+  const int32_t xt_off = PL ? 0 : a.xt_off;   // split basin: the export-row table
   const bool force_to = a.flags & kFlagForceTimeout;
   R* xsave = static_cast<R*>(a.x_save);
   const int TTf = (int)T + B.dmax;
@@ -538,9 +545,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // runoff (N, T) written from here: the last four steps of each reach, stored 16 B at a time
   R ob0[KR], ob1[KR], ob2[KR], ob3[KR];
   R* runoff = static_cast<R*>(a.runoff);
-  const bool emit = runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
+  const bool emit = PL == 1 || (PL == 0 && runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF));
   // rows 16-B aligned: vector stores (per-step 4-B stores measured 1.6x slower for the whole kernel)
-  const bool emit4 = (T & 3) == 0;
+  const bool emit4 = PL == 1 || (T & 3) == 0;
   // Storer waves (one reach per thread, blocks of at most half a workgroup): the idle upper half of the
   // workgroup stores each reach's published x (x_save row, runoff) during the next tick, so a compute
   // wave's top-of-tick wait covers only its q' prefetch -- not the acknowledgement of its stores, which
@@ -606,8 +613,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   load_math_tables();
   load_xlist(a, B, xl);
-  uintptr_t* xt = reinterpret_cast<uintptr_t*>(smem + a.xt_off);  // split: cut-outs' export rows
-  if (a.xt_off) {
+  uintptr_t* xt = reinterpret_cast<uintptr_t*>(smem + xt_off);  // split: cut-outs' export rows
+  if (xt_off) {
     for (int c = tid; c < B.ncout; c += BS) {
       const int64_t e = B.cout0 + c;
       const int xi = a.xid[e];
@@ -617,14 +624,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   __syncthreads();
   unsigned long long prof_wait = 0;
-  if (a.prof && tid == 0) prof_begin(a.prof, bid);
+  if (aprof && tid == 0) prof_begin(aprof, bid);
   PhaseProf phz;
   phz.start();
 
   // q'[max(t-1,0)] * flow_scale (gathered into the schedule layout: one row per tick), or the
   // carried Q0 at t = 0, for the step each reach runs at tick `tau`
   const R* qsb = static_cast<const R*>(a.qs) + xs_base;
-  const bool qs_rows = a.qs_rows > 0;
+  const bool qs_rows = PL == 4 || (PL == 0 && a.qs_rows > 0);
   // kSt (steady ticks, below): no reach is at its carried t = 0 step
   auto prefetch = [&](int tau, R(&dst)[KR], int tq0, auto sc) {
     constexpr bool kSt = decltype(sc)::value;
@@ -653,7 +660,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const R xr = R(xd);
     if (DDR_FWD_STORER_GRANULES && B.ncout > 0 && (so >> 16)) {
       const int64_t e = B.cout0 + (so >> 16) - 1;
-      if (a.xt_off) {
+      if (xt_off) {
         const uintptr_t p = xt[(so >> 16) - 1];
         double* row = reinterpret_cast<double*>(p & ~uintptr_t(1));
         if (p & 1u) store_granule_sys(row + t, xd);
@@ -679,13 +686,13 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if (B.nvirt > 0 && (tau % kChunkFwd) == 0) {
       // import the next chunk of every virtual inflow (x of the upstream block's reach): its owner
       // thread requests the kChunkFwd granules at once
-      const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+      const unsigned long long w0 = aprof ? __builtin_amdgcn_s_memrealtime() : 0;
       if (kPrefImport && vown) {
         // (light and medium loads) the chunk was requested one chunk ago: its granules have landed while
         // the block ran, so the import waits only for those still unpublished, and the next chunk is
         // requested now -- the owner's wave (and the barrier after it) no longer pays a memory round
         // trip every kChunkFwd ticks
-        const int xi = a.xid ? a.xid[v_edge] : -1;  // split basin: another rank's block, receive rows
+        const int xi = (!PL && a.xid) ? a.xid[v_edge] : -1;  // split basin: another rank's block, receive rows
         const double* row = xi >= 0 ? a.xfwd + (int64_t)xi * T : a.bnd + (int64_t)v_edge * T;
         const int64_t t0 = (int64_t)tau - v_off;
         double g[kChunkFwd];
@@ -702,7 +709,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         for (int i = 0; i < kChunkFwd; ++i) ring[vi * kChunkFwd + i] = g[i];
       } else if (vown) {
         // split basin: a cut edge from another rank's block arrives in this rank's receive rows
-        const int xi = a.xid ? a.xid[v_edge] : -1;
+        const int xi = (!PL && a.xid) ? a.xid[v_edge] : -1;
         if (xi >= 0) {
 #pragma unroll
           for (int h = 0; h < kChunkFwd; h += kImportBatch) {
@@ -727,7 +734,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #define DDR_FWD_IMPORT_BARRIER 0
 #endif
       if (DDR_FWD_IMPORT_BARRIER) lds_barrier();
-      if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
+      if (aprof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
   };
   // a virtual inflow's value of tick tau into its slot of buffer `dst` (owners only)
@@ -894,7 +901,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           }
           if (B.ncout > 0 && (off[k] >> 16) && !(DDR_FWD_STORER_GRANULES && storer_mode)) {
             const int64_t e = B.cout0 + (off[k] >> 16) - 1;
-            if (a.xt_off) {  // split basin: the row from the block's table (another rank's: system scope)
+            if (xt_off) {  // split basin: the row from the block's table (another rank's: system scope)
               const uintptr_t p = xt[(off[k] >> 16) - 1];
               double* row = reinterpret_cast<double*>(p & ~uintptr_t(1));
               if (p & 1u) store_granule_sys(row + t, x);
@@ -974,19 +981,19 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if (!DDR_FWD_STEADY || (a.flags & kFlagNoSteady) || accum || s1 <= s0) s0 = s1 = 0;
 #pragma unroll 1
   for (int tau = 0; tau < s0; tau += 2) {
-    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    if (aprof && tid == 0) prof_tick(aprof, bid, tau);
     tick(tau, qa, qb, Gen{});
     tick(tau + 1, qb, qa, Gen{});
   }
 #pragma unroll 1
   for (int tau = s0; tau < s1; tau += 2) {
-    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    if (aprof && tid == 0) prof_tick(aprof, bid, tau);
     tick(tau, qa, qb, Steady{});
     tick(tau + 1, qb, qa, Steady{});
   }
 #pragma unroll 1
   for (int tau = s1; tau < TT; tau += 2) {
-    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    if (aprof && tid == 0) prof_tick(aprof, bid, tau);
     tick(tau, qa, qb, Gen{});
     if (tau + 1 < TT) tick(tau + 1, qb, qa, Gen{});
   }
@@ -994,14 +1001,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
 #pragma unroll 1
   for (int tau = 0; tau < TT; ++tau) {
-    if (a.prof && tid == 0) prof_tick(a.prof, bid, tau);
+    if (aprof && tid == 0) prof_tick(aprof, bid, tau);
     tick(tau, qa, qb, Gen{});
 #pragma unroll
     for (int k = 0; k < KR; ++k) qa[k] = qb[k];
   }
 #endif
-  if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
-  phz.flush(a.prof, a.nblocks, bid);
+  if (aprof && tid == 0) prof_end(aprof, bid, prof_wait);
+  phz.flush(aprof, a.nblocks, bid);
 }
 
 // The forward's last-step outputs (mmc.py:441 _discharge_t, mmc.py:161-162 top_width / side_slope), from
@@ -1117,7 +1124,9 @@ __device__ __forceinline__ Grad4<R> make_grad4(R a, R b, R c, R d) { return Grad
 // of every step (gb c4 [q' >= q_lb], mmc.py:421-424, 535-538) into gqs, the schedule layout of qs.
 // XB: the slot buffers when not the KR rule's (bwd_xbuf): 1 = single-buffered slots where the double buffer
 // does not fit the LDS (fp64 at KR = 2, bwd_xb_of)
-template <typename R, int KR, bool GS, int XB = 0, bool DF = false>
+// PL (plain, as the forward's): no split basin, no profile, no state seeds, 16-B (N, T) rows; 1: dL/drunoff per
+// reach, 2: gauge mode -- the tests of those options and the uniform values behind them leave the tick loop
+template <typename R, int KR, bool GS, int XB = 0, bool DF = false, int PL = 0>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_backward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1149,7 +1158,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const R* gout = static_cast<const R*>(a.grad_out);
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
-  const bool vec4 = (T & 3) == 0;               // (N, T) rows 16-B aligned
+  const bool vec4 = PL || (T & 3) == 0;         // (N, T) rows 16-B aligned
+  const bool gauge = PL == 2 || (PL == 0 && a.g_roff != nullptr);  // dL/dout per gauge (G, T)
+  const void* const gseed = PL ? nullptr : a.gseed;                 // state seeds of steps T - 1, T - 2
+  unsigned long long* const aprof = PL ? nullptr : a.prof;
+  const int32_t xt_off = PL ? 0 : a.xt_off;
   const int tmin = GS ? 0 : 1;                  // first step of the sweep (step 0: the hot start / Q0)
   R* gqs = static_cast<R*>(a.gqs);
 
@@ -1210,10 +1223,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     const bool hk = r < B.nloc;
     const int P = B.pos0 + (hk ? r : 0);
     ref[k] = a.s.ref[P];
-    const bool nograd = a.g_roff != nullptr && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]] && a.gseed == nullptr;
+    const bool nograd = gauge && a.g_roff[ref[k] + 1] == a.g_roff[ref[k]] && gseed == nullptr;
     if constexpr (kGReg) {
       gsg[k] = -1;
-      if (a.g_roff != nullptr && a.g_roff[ref[k] + 1] - a.g_roff[ref[k]] == 1) gsg[k] = (int)a.g_rg[a.g_roff[ref[k]]];
+      if (gauge && a.g_roff[ref[k] + 1] - a.g_roff[ref[k]] == 1) gsg[k] = (int)a.g_rg[a.g_roff[ref[k]]];
     }
     od[k] = ((unsigned)a.s.off[P] << 16) | ((unsigned)a.s.dloc[P] & 0xFFFFu) | (nograd ? 0x80000000u : 0u);
     up[k] = pack_up(a, P, (unsigned)(S - 1));  // slot S-1 holds 0: missing upstreams add exactly 0
@@ -1280,9 +1293,9 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   load_xlist(a, B, xl);
   // split basin: [nvirt] the virtuals' export rows (to the producer block's rank), then [ncout] the
   // cut-outs' import rows (this rank's receive rows for edges from another rank's consumer)
-  uintptr_t* xtv = reinterpret_cast<uintptr_t*>(smem + a.xt_off);
+  uintptr_t* xtv = reinterpret_cast<uintptr_t*>(smem + xt_off);
   uintptr_t* xtc = xtv + B.nvirt;
-  if (a.xt_off) {
+  if (xt_off) {
     for (int v = tid; v < B.nvirt; v += BS) {
       const int64_t e = a.s.v_edge[B.virt0 + v];
       const int xi = a.xid[e];
@@ -1298,7 +1311,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   __syncthreads();
   unsigned long long prof_wait = 0;
-  if (a.prof && tid == 0) prof_begin(a.prof, bid);
+  if (aprof && tid == 0) prof_begin(aprof, bid);
   PhaseProf phz;
 
   // x of this reach at forward tick `tau` (clamped into the block's rows)
@@ -1315,7 +1328,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // boundary granules (t clamped into [0, T))
   // split basin: a virtual whose producer is another rank's block sends its x to this rank's receive rows;
   // split_finish_kernel copied them into this call's bnd after the forward
-  const int vxi = (vown && a.xid) ? a.xid[v_edge] : -1;  // split basin: the virtual's cross-rank row
+  const int vxi = (!PL && vown && a.xid) ? a.xid[v_edge] : -1;  // split basin: the virtual's cross-rank row
   auto load_virt = [&](int64_t t) -> double {
     const int64_t tc = t < 0 ? 0 : (t >= T ? T - 1 : t);
     return a.bnd[(int64_t)v_edge * T + tc];
@@ -1367,7 +1380,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       return make_grad4(row[i0], row[i1], row[i2], row[i3]);
     };
-    if (a.g_roff) {
+    if (gauge) {
       const bool z = GS && a.gmask0 && base <= 0;  // the group holds step 0
       if (gs >= 0) {
         // the reach's only gauge (kGReg): the row address needs no dependent index loads in the tick
@@ -1402,8 +1415,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // loop's code and registers are those of an unseeded launch
   auto load_grad = [&](int ref, int64_t base, int gs, bool seeded) {
     Grad4<R> v = load_grad_out(ref, base, gs, seeded);
-    if (seeded && a.gseed != nullptr && base + 3 >= T - 2) {
-      const R* sd = static_cast<const R*>(a.gseed);
+    if (seeded && gseed != nullptr && base + 3 >= T - 2) {
+      const R* sd = static_cast<const R*>(gseed);
       const R s1 = sd[ref], s2 = sd[a.N + ref];
       auto add = [&](R& g, int64_t t) { g = g + (t == T - 1 ? s1 : (t == T - 2 ? s2 : R(0))); };
       add(v.a, base);
@@ -1457,14 +1470,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       // one (cut-out, step) per thread and iteration, its (A, B) granule pair requested together; the
       // cut edge of cut-out c is B.cout0 + c (graph.cpp numbers cut edges in block order), its tick
       // offset is in the owner words
-      const unsigned long long w0 = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+      const unsigned long long w0 = aprof ? __builtin_amdgcn_s_memrealtime() : 0;
       for (int w = tid; !imp_mode && w < B.ncout * kChunkBwd; w += BS) {
         const int c = w / kChunkBwd, sidx = w % kChunkBwd;
         const int t = (tau - sidx) - (int)(own[c] >> 16);
         R A = R(0), Bv = R(0);
         if (t >= tmin && t < T) {
           double g[2];
-          const uintptr_t p = a.xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
+          const uintptr_t p = xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
           const double* row = reinterpret_cast<const double*>(p & ~uintptr_t(1)) + (int64_t)t * 2;
           if (p & 1u) wait_granules<2, true>(row, 0, 1, 0, 2, g, a.status, bid, force_to);  // another rank's consumer
           else wait_granules<2>(row, 0, 1, 0, 2, g, a.status, bid, force_to);
@@ -1475,7 +1488,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         ring[(c * kChunkBwd + sidx) * 2 + 1] = Bv;
       }
       lds_barrier();
-      if (a.prof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
+      if (aprof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
     phz.mark(1);  // import
     // ---- read / publish ----------------------------------------------------------------------
@@ -1638,7 +1651,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if (carry) {
           // Q0 = q0 feeds step 1 unclamped; runoff[:, 0] = clamp(q0) per reach, or the gauge sum's clamp
           // (already folded into gk through gmask0)
-          if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = a.g_roff ? P.lm : lam[k] + ((P.xtk >= cs.qlb) ? P.gk : R(0));
+          if (a.gq0) static_cast<R*>(a.gq0)[ref[k]] = gauge ? P.lm : lam[k] + ((P.xtk >= cs.qlb) ? P.gk : R(0));
           gqs[xs_base + (int64_t)tau * B.nloc + r] = R(0);
           saw[r] = R(0);
           sbw[r] = R(0);
@@ -1788,7 +1801,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
     for (int i = 0; i < XD; ++i) xp[i] = xload(i);
     const int c = wown ? w / kChunkBwd : 0, sidx = w % kChunkBwd;
-    const uintptr_t p = !wown ? 0 : a.xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
+    const uintptr_t p = !wown ? 0 : xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
     const bool sys = p & 1u;
     const double* prow = reinterpret_cast<const double*>(p & ~uintptr_t(1));
     const int coff = wown ? (int)(own[c] >> 16) : 0;
@@ -1850,7 +1863,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // steady backward ticks [b0, b1): forward ticks tau = TT - 1 - tb in [dmax + 2, T - 1]
   // (state seeds: from forward tick T - 2 down, so that every load of the groups of steps T - 2 and T - 1 --
   // issued at forward ticks >= T - 1 -- runs in a general tick)
-  int b0 = a.gseed != nullptr ? B.dmax + 1 : B.dmax, b1 = (int)T - 2;
+  int b0 = gseed != nullptr ? B.dmax + 1 : B.dmax, b1 = (int)T - 2;
   if (kEarly) {  // even bounds: the register roles keep alternating
     b0 += b0 & 1;
     b1 &= ~1;
@@ -1859,41 +1872,41 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   if constexpr (kEarly) {
 #pragma unroll 1
     for (int tb = 0; tb < b0; tb += 2) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb2, vx, vx2, Gen{});
       tick(tb + 1, xb2, xb, vx2, vx, Gen{});
     }
 #pragma unroll 1
     for (int tb = b0; tb < b1; tb += 2) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb2, vx, vx2, Steady{});
       tick(tb + 1, xb2, xb, vx2, vx, Steady{});
     }
 #pragma unroll 1
     for (int tb = b1; tb < TT; tb += 2) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb2, vx, vx2, Gen{});
       if (tb + 1 < TT) tick(tb + 1, xb2, xb, vx2, vx, Gen{});
     }
   } else {
 #pragma unroll 1
     for (int tb = 0; tb < b0; ++tb) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb, vx, vx, Gen{});
     }
 #pragma unroll 1
     for (int tb = b0; tb < b1; ++tb) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb, vx, vx, Steady{});
     }
 #pragma unroll 1
     for (int tb = b1; tb < TT; ++tb) {
-      if (a.prof && tid == 0) prof_tick(a.prof, bid, tb);
+      if (aprof && tid == 0) prof_tick(aprof, bid, tb);
       tick(tb, xb, xb, vx, vx, Gen{});
     }
   }
-  if (a.prof && tid == 0) prof_end(a.prof, bid, prof_wait);
-  phz.flush(a.prof, a.nblocks, bid);
+  if (aprof && tid == 0) prof_end(aprof, bid, prof_wait);
+  phz.flush(aprof, a.nblocks, bid);
 }
 
 // Final fp64 accumulators -> R gradients (reference order).
@@ -2196,7 +2209,7 @@ size_t route_smem_bytes(const Graph* g, bool backward) {
 // the backward kernel of this launch (state gradients: GS; single-buffered fp64 KR = 2 slots: bwd_xb_of)
 // (exact adjoint of the fp32 trajectory, DDR_BWD_EXACT_ADJOINT: df)
 template <typename R, int KR>
-const void* backward_kernel_of(const Graph* g, bool gs, bool df = false) {
+const void* backward_kernel_of(const Graph* g, bool gs, bool df = false, int pl = 0) {
   if constexpr (KR == 2 && sizeof(R) == 8) {
     if (bwd_xb_of<R>(g) == 1)
       return gs ? (const void*)route_backward_kernel<R, KR, true, 1> : (const void*)route_backward_kernel<R, KR, false, 1>;
@@ -2206,7 +2219,32 @@ const void* backward_kernel_of(const Graph* g, bool gs, bool df = false) {
       return gs ? (const void*)route_backward_kernel<R, KR, true, 0, true>
                 : (const void*)route_backward_kernel<R, KR, false, 0, true>;
   }
+  if constexpr (sizeof(R) == 4) {
+    if (!gs && pl == 2) return (const void*)route_backward_kernel<R, KR, false, 0, false, 2>;
+  }
   return gs ? (const void*)route_backward_kernel<R, KR, true> : (const void*)route_backward_kernel<R, KR, false>;
+}
+// the plain backward instance a launch can take (route_backward_kernel's PL), 0 when none
+inline int backward_plain_of(const Graph* g, const RouteArgs& a) {
+  static const bool ok = [] {
+    const char* v = getenv("DDR_BWD_PLAIN");
+    return v == nullptr || atoi(v) != 0;
+  }();
+  if (!ok || g->split.nranks > 0 || a.prof != nullptr || a.gseed != nullptr || (a.T & 3) != 0) return 0;
+  // gauge mode only: c3s8 backward -4.5 %; per-reach dL/drunoff (PL = 1) measured 1-2 % slower at C5 and at
+  // light load (r05_plain3), so that instance is not taken
+  return a.g_roff != nullptr ? 2 : 0;
+}
+
+// the faithful forward instance for a plain code (route_forward_kernel's PL; 0: the general one)
+template <typename R, int KR, int XB>
+auto forward_faithful_of(int pl) {
+  switch (pl) {
+    case 1: return route_forward_kernel<R, KR, 2, XB, 1>;
+    case 2: return route_forward_kernel<R, KR, 2, XB, 2>;
+    case 4: return route_forward_kernel<R, KR, 2, XB, 4>;
+    default: return route_forward_kernel<R, KR, 2, XB>;
+  }
 }
 
 template <typename R, int KR>
@@ -2221,7 +2259,8 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
   a.xt_off = g->split.nranks > 0 ? (int32_t)align16(base) : 0;
   const dim3 grid((unsigned)g->blocks.size()), block(kBlockThreads);
   if (backward) {
-    const void* kern = backward_kernel_of<R, KR>(g, a.gqs != nullptr, (a.flags & DDR_BWD_EXACT_ADJOINT) != 0);
+    const void* kern = backward_kernel_of<R, KR>(g, a.gqs != nullptr, (a.flags & DDR_BWD_EXACT_ADJOINT) != 0,
+                                                  backward_plain_of(g, a));
     hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     void* kargs[] = {&a};
@@ -2236,8 +2275,19 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
     auto kern = route_forward_kernel<R, KR, 0>;
     size_t fsmem = smem;
     if constexpr (std::is_same<R, float>::value) {
+      // the plain instance (route_forward_kernel's PL) this launch can take: 0 none, 1 runoff rows, 2 none written
+      static const bool plain_ok = [] {
+        const char* v = getenv("DDR_FWD_PLAIN");
+        return v == nullptr || atoi(v) != 0;
+      }();
+      const bool rows = a.runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
+      int plain = 0;
+      if (plain_ok && g->split.nranks == 0 && a.prof == nullptr && !(a.flags & DDR_FWD_ACCUMULATE)) {
+        if (rows) plain = ((a.T & 3) == 0 && a.qs_rows <= 0) ? 1 : 0;
+        else plain = a.qs_rows > 0 ? 4 : 2;
+      }
       if (a.flags & DDR_FWD_FAST_MATH) kern = route_forward_kernel<R, KR, 1>;
-      else if (a.flags & DDR_FWD_FAITHFUL_MATH) kern = route_forward_kernel<R, KR, 2>;
+      else if (a.flags & DDR_FWD_FAITHFUL_MATH) kern = forward_faithful_of<R, KR, 0>(plain);
       // KR = 4 (faithful): double-buffered x slots -- one barrier per tick -- where this graph's largest
       // block leaves the LDS for a second buffer (C5's blocks of <= ~3800 reaches; C3's 4096 do not)
       if constexpr (KR == 4) {
@@ -2249,7 +2299,7 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
                                           (size_t)g->max_cout, (size_t)g->max_xl, false, sizeof(R), g->kr, 2);
         const size_t s2 = align16(b2) + split_table_bytes(g, false);
         if (dbl4 && (a.flags & DDR_FWD_FAITHFUL_MATH) && s2 <= kLdsBudget) {
-          kern = route_forward_kernel<R, KR, 2, 2>;
+          kern = forward_faithful_of<R, KR, 2>(plain);
           fsmem = s2;
           a.xl_off = (int32_t)(b2 - (size_t)g->max_xl * 4);
           a.own_off = a.xl_off - (int32_t)align16(4 * (size_t)std::max(g->max_virt, g->max_cout));
