@@ -1159,10 +1159,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const int64_t xs_base = T * B.pos0 + B.pre_dn;
   double* gacc = a.bwd_bnd + 2 * a.n_cut * T;  // (N, 3) fp64 gradient accumulators (zeroed)
   const bool vec4 = PL || (T & 3) == 0;         // (N, T) rows 16-B aligned
-  const bool gauge = PL == 2 || (PL == 0 && a.g_roff != nullptr);  // dL/dout per gauge (G, T)
-  const void* const gseed = PL ? nullptr : a.gseed;                 // state seeds of steps T - 1, T - 2
-  unsigned long long* const aprof = PL ? nullptr : a.prof;
-  const int32_t xt_off = PL ? 0 : a.xt_off;
+  // (expressions at each use, not locals: the general instance then keeps the code and registers it had
+  // before the plain ones existed -- locals held across the tick loop spill at KR = 4)
+#define gauge (PL == 2 || (PL == 0 && a.g_roff != nullptr))  // dL/dout per gauge (G, T)
+#define gseed (PL ? nullptr : a.gseed)                        // state seeds of steps T - 1, T - 2
+#define aprof (PL ? nullptr : a.prof)
+#define xt_off (PL ? 0 : a.xt_off)
   const int tmin = GS ? 0 : 1;                  // first step of the sweep (step 0: the hot start / Q0)
   R* gqs = static_cast<R*>(a.gqs);
 
@@ -1907,6 +1909,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   if (aprof && tid == 0) prof_end(aprof, bid, prof_wait);
   phz.flush(aprof, a.nblocks, bid);
+#undef gauge
+#undef gseed
+#undef aprof
+#undef xt_off
 }
 
 // Final fp64 accumulators -> R gradients (reference order).
@@ -2231,8 +2237,8 @@ inline int backward_plain_of(const Graph* g, const RouteArgs& a) {
     return v == nullptr || atoi(v) != 0;
   }();
   if (!ok || g->split.nranks > 0 || a.prof != nullptr || a.gseed != nullptr || (a.T & 3) != 0) return 0;
-  // gauge mode only: c3s8 backward -4.5 %; per-reach dL/drunoff (PL = 1) measured 1-2 % slower at C5 and at
-  // light load (r05_plain3), so that instance is not taken
+  // gauge mode only: c3s8 backward -4.5 %; per-reach dL/drunoff (PL = 1) measured 0.5-1.5 % slower at C5 and
+  // 3 % at light load (r05_plain3, r05_pl1), so that instance is not built
   return a.g_roff != nullptr ? 2 : 0;
 }
 
