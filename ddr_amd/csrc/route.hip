@@ -1277,6 +1277,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #define DDR_BWD_XHELP_D 3
 #endif
   const bool xhelp = help_ok && DDR_BWD_XHELP;
+  // gradient helpers (x-helper blocks, per-reach dL/drunoff, statics in registers): the same upper waves also
+  // load each reach's dL/drunoff[:, t] DDR_BWD_XHELP_D ticks ahead and publish it into a parity-indexed LDS row
+  // (the statics table's space, unused when the statics live in registers), so the routing waves issue no
+  // global load and wait for none at the tick's top (a cold 16-B group load, one tick ahead, paced the light
+  // backward: profiles/r05/ab_r05.txt item 12)
+#ifndef DDR_BWD_GHELP
+#define DDR_BWD_GHELP 1
+#endif
+  const bool ghelp = DDR_BWD_GHELP && kStatReg && kShiftG && xhelp && !(gauge);
+  R* const sg = reinterpret_cast<R*>(sx + kXB * S);  // [2][S] (ghelp): dL/drunoff of each reach's step, by tick parity
   // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
   // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
   // tid < ncout: its import owner)
@@ -1426,6 +1436,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       add(v.c, base + 2);
       add(v.d, base + 3);
     }
+    return v;
+  };
+
+  // (ghelp) the value helper w publishes at backward tick tb, read by its reach at tick tb + 1: dL/drunoff of the
+  // step t = TT - 2 - tb - off (0 outside [0, T)), plus the state seeds of steps T - 1 and T - 2
+  // (rf, off: reach w's reference index and tick offset, loaded once)
+  auto ghelp_load = [&](int rf, int off, int tb) -> R {
+    const int64_t t = (int64_t)TT - 2 - tb - off;
+    if (t < 0 || t >= T) return R(0);
+    R v = gout[(int64_t)rf * T + t];
+    if (gseed != nullptr && t >= T - 2) v = v + static_cast<const R*>(gseed)[(t == T - 1 ? 0 : a.N) + rf];
     return v;
   };
 
@@ -1586,6 +1607,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         g3[k] = g2[k];
         g2[k] = g1[k];
         g1[k] = g0[k];
+        if (kStatReg && ghelp) P.gk = sg[(tb & 1) * S + P.rs];  // published by the gradient helpers last tick
       } else {
         const int e4 = P.t & 3;
         if constexpr (DDR_BWD_SEL_BITS) {
@@ -1672,7 +1694,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
       // dL/drunoff of the next step's group, one tick ahead
       const int tn = P.t - 1;
-      if (P.hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
+      if (!ghelp && P.hk && has_grad(k) && (kSt ? (tn & 3) == 3 : (tn >= 0 && tn < T && ((tn & 3) == 3 || tn == T - 1)))) {
         const Grad4<R> v = load_grad(ref[k], kShiftG ? (int64_t)tn - 3 : (int64_t)(tn & ~3),
                                      kGReg ? opq(gsg[kGReg ? k : 0]) : -1, !kSt);
         g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
@@ -1776,11 +1798,16 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if (vown) sx[B.nloc + tid] = R(vx);
     load_own(TT - 4, xb, tid);
     if (vown) vx = load_virt((int64_t)(TT - 2) - v_off - 2);
+    // (ghelp) tick 0's dL/drunoff row, written by the helper thread of each reach
+    if (ghelp && tid >= BS / 2 && tid - BS / 2 < B.nloc) {
+      const int P = B.pos0 + tid - BS / 2;
+      sg[tid - BS / 2] = ghelp_load(a.s.ref[P], a.s.off[P], -1);
+    }
     __syncthreads();
   }
 #pragma unroll
   for (int k = 0; k < KR; ++k)
-    if (tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
+    if (!ghelp && tid + k * BS < B.nloc && has_grad(k) && TT - 1 - off_of(k) == T - 1) {
       const Grad4<R> v = load_grad(ref[k], kShiftG ? T - 4 : (T - 1) & ~int64_t(3), kGReg ? gsg[kGReg ? k : 0] : -1, true);
       g0[k] = v.a; g1[k] = v.b; g2[k] = v.c; g3[k] = v.d;
     }
@@ -1799,9 +1826,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       tc = tc < 0 ? 0 : (tc >= TT ? TT - 1 : tc);
       return xown ? xcol[(int64_t)tc * B.nloc] : R(0);
     };
-    R xp[XD];
+    R xp[XD], gp[XD];
+    const bool gown = ghelp && w < B.nloc;
+    const int grf = gown ? a.s.ref[B.pos0 + w] : 0, goff = gown ? a.s.off[B.pos0 + w] : 0;
 #pragma unroll
-    for (int i = 0; i < XD; ++i) xp[i] = xload(i);
+    for (int i = 0; i < XD; ++i) {
+      xp[i] = xload(i);
+      gp[i] = gown ? ghelp_load(grf, goff, i) : R(0);
+    }
     const int c = wown ? w / kChunkBwd : 0, sidx = w % kChunkBwd;
     const uintptr_t p = !wown ? 0 : xt_off ? xtc[c] : reinterpret_cast<uintptr_t>(a.bwd_bnd + (int64_t)(B.cout0 + c) * T * 2);
     const bool sys = p & 1u;
@@ -1810,7 +1842,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     auto step_of = [&](int tb) { return (TT - 1 - tb - sidx) - coff; };  // the step chunk tb's slot needs
     unsigned long long eg[2] = {0ull, 0ull};
     bool issued = false;
-    auto htick = [&](int tb, R& xr) {
+    auto htick = [&](int tb, R& xr, R& gr) {
       if (B.ncout > 0 && (tb % kChunkBwd) == 0) {
         if (wown) {
           const int t = step_of(tb);
@@ -1838,6 +1870,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         sx[((tb + 1) & 1) * S + w] = xr;  // the routing waves read it next tick
         xr = xload(tb + XD);
       }
+      if (gown) {
+        sg[((tb + 1) & 1) * S + w] = gr;
+        gr = ghelp_load(grf, goff, tb + XD);
+      }
       const int nb = tb + DDR_BWD_IMP_EARLY;
       if (DDR_BWD_IMP_EARLY > 0 && wown && (nb % kChunkBwd) == 0 && nb < TT) {
         const int t = step_of(nb);
@@ -1855,7 +1891,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int tb = 0; tb < TT; tb += XD) {
 #pragma unroll
       for (int i = 0; i < XD; ++i)
-        if (tb + i < TT) htick(tb + i, xp[i]);
+        if (tb + i < TT) htick(tb + i, xp[i], gp[i]);
     }
     return;
   }
