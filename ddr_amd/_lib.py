@@ -44,6 +44,7 @@ DDR_BWD_EXACT_ADJOINT = 128
 DDR_DEBUG_FORCE_TIMEOUT = 1
 DDR_DEBUG_NO_STEADY = 2
 DDR_DEBUG_NO_STORER = 4
+DDR_DEBUG_NO_PLAIN = 8
 
 
 class BuildOpts(C.Structure):

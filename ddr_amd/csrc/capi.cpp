@@ -46,9 +46,12 @@ struct KernelTiming {
 } g_timing;
 unsigned long long* g_prof[2] = {nullptr, nullptr};
 int32_t g_debug = [] {  // ddr_set_debug_flags (DDR_NO_STEADY=1: the general tick path only, for A/B)
-  const char* e = std::getenv("DDR_NO_STEADY");
-  const char* f = std::getenv("DDR_NO_STORER");
-  return ((e && e[0] == '1') ? kFlagNoSteady : 0) | ((f && f[0] == '1') ? kFlagNoStorer : 0);
+  auto on = [](const char* name) {
+    const char* v = std::getenv(name);
+    return v && v[0] == '1';
+  };
+  return (on("DDR_NO_STEADY") ? kFlagNoSteady : 0) | (on("DDR_NO_STORER") ? kFlagNoStorer : 0) |
+         (on("DDR_NO_PLAIN") ? kFlagNoPlain : 0);
 }();
 
 // Hand-off failures surface without a host sync on the hot path: after every routing launch the
@@ -187,7 +190,25 @@ bool capturing(hipStream_t s) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
-hipError_t ready_for(const Graph* g, hipStream_t s) { return capturing(s) ? hipSuccess : graph_ready(g, s); }
+// Order `s` after the graph's build.  A capture cannot wait on the upload event (recorded outside it), so a
+// device- or stream-built graph whose completion no launch outside a capture has waited for yet is refused
+// there: its first replay could read a half-uploaded schedule.
+ddr_status ready_for(const Graph* g, hipStream_t s) {
+  if (capturing(s)) {
+    if (g->ready && !g->ready_waited.load(std::memory_order_acquire))
+      return fail(DDR_ERR_ARG, "graph used inside a stream capture before any launch outside it waited for its build: "
+                               "route with it once outside the capture first");
+    return DDR_OK;
+  }
+  DDR_HIP(graph_ready(g, s));
+  g->ready_waited.store(true, std::memory_order_release);
+  return DDR_OK;
+}
+#define DDR_TRY(call)                   \
+  do {                                  \
+    const ddr_status _st = (call);      \
+    if (_st != DDR_OK) return _st;      \
+  } while (0)
 
 hipError_t timing_mark(int which, int edge, hipStream_t s) {
   if (!g_timing.on || capturing(s)) return hipSuccess;
@@ -323,7 +344,7 @@ ddr_status forward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_m
     return fail(DDR_ERR_ARG, "stream capture: split-basin launches and the q' NaN check cannot be captured");
   if (!cap && (st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, false))) return st;
-  DDR_HIP(ready_for(g, s));
+  DDR_TRY(ready_for(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bnd, 0xFF, sizeof(double) * g->n_cut * T, s));
   RouteArgs a;
@@ -389,7 +410,7 @@ ddr_status backward_impl(const ddr_graph* gh, const ddr_mc_consts* c, const ddr_
   if (cap && g->split.nranks > 0) return fail(DDR_ERR_ARG, "stream capture: split-basin launches cannot be captured");
   if (!cap && (st = g_pending.check(false))) return st;
   if ((st = check_launchable<R>(g, true))) return st;
-  DDR_HIP(ready_for(g, s));
+  DDR_TRY(ready_for(g, s));
   DDR_HIP(hipMemsetAsync(status, 0, kStatusBytes, s));
   if (g->n_cut > 0) DDR_HIP(hipMemsetAsync(bwd_bnd, 0xFF, sizeof(double) * 2 * g->n_cut * T, s));
   DDR_HIP(hipMemsetAsync(bwd_bnd + 2 * g->n_cut * T, 0, sizeof(double) * 3 * g->n, s));
@@ -458,7 +479,7 @@ ddr_status gauge_impl(const ddr_graph* gh, const R* x_save, int64_t T, const ddr
   ddr_status st = gauge_args<R>(gh, x_save, T, gz, qlb, flags, a);
   if (st) return st;
   if (!out) return fail(DDR_ERR_ARG, "null gauge output");
-  DDR_HIP(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
+  DDR_TRY(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge<R>(a, x_save, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -477,7 +498,7 @@ ddr_status gauge_daily_impl(const ddr_graph* gh, const R* x_save, int64_t T, con
   if (st) return st;
   if ((st = check_window(T, t0, L, D))) return st;
   if (!out) return fail(DDR_ERR_ARG, "null daily output");
-  DDR_HIP(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
+  DDR_TRY(ready_for(reinterpret_cast<const Graph*>(gh), static_cast<hipStream_t>(stream)));
   DDR_HIP(launch_gauge_daily<R>(a, x_save, t0, L, D, out, static_cast<hipStream_t>(stream)));
   return DDR_OK;
 }
@@ -557,7 +578,7 @@ ddr_status state_impl(const ddr_graph* gh, const R* x_save, int64_t T, int64_t t
   // a split rank holds the states of its own blocks only
   if (g->split.nranks > 0) return fail(DDR_ERR_ARG, "split basin: the saved states are per rank");
   hipStream_t s = static_cast<hipStream_t>(stream);
-  DDR_HIP(ready_for(g, s));
+  DDR_TRY(ready_for(g, s));
   DDR_HIP(launch_state_at<R>(g, T, t, qlb, (flags & DDR_FWD_CARRY) != 0, x_save, out, s));
   return DDR_OK;
 }
@@ -1134,7 +1155,7 @@ ddr_status ddr_status_check(int32_t wait) {
 
 ddr_status ddr_set_debug_flags(int32_t flags) {
   g_debug = ((flags & DDR_DEBUG_FORCE_TIMEOUT) ? kFlagForceTimeout : 0) | ((flags & DDR_DEBUG_NO_STEADY) ? kFlagNoSteady : 0) |
-            ((flags & DDR_DEBUG_NO_STORER) ? kFlagNoStorer : 0);
+            ((flags & DDR_DEBUG_NO_STORER) ? kFlagNoStorer : 0) | ((flags & DDR_DEBUG_NO_PLAIN) ? kFlagNoPlain : 0);
   return DDR_OK;
 }
 

@@ -141,40 +141,6 @@ __device__ __forceinline__ float pow_faithful(float x, float y) {
   return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f), (int)ip);
 }
 
-// ---- packed pairs: two evaluations in the halves of a float2, the FMA / multiply / add steps as one
-// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 each (IEEE fp32 per half: the same bits as the scalar
-// forms), the transcendental, integer and select steps per half ----
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 mk2(float a, float b) { return f2{a, b}; }
-__device__ __forceinline__ f2 sp2(float a) { return f2{a, a}; }
-__device__ __forceinline__ f2 rcp2(f2 b) { return f2{__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)}; }
-// div_rn on both halves (the same operations)
-__device__ __forceinline__ f2 div_rn2(f2 a, f2 b) {
-  f2 y = rcp2(b);
-  const f2 e = fma2(-b, y, sp2(1.0f));
-  y = fma2(e, y, y);
-  const f2 q = a * y;
-  const f2 r = fma2(-q, b, a);
-  return fma2(r, y, q);
-}
-// pow_faithful on both halves (the same operations)
-__device__ __forceinline__ f2 pow_faithful2(f2 x, f2 y) {
-  const int ux = __float_as_int(x.x), uy = __float_as_int(x.y);
-  const int ex = (ux - 0x3F3504F3) >> 23, ey = (uy - 0x3F3504F3) >> 23;
-  const f2 m = mk2(__int_as_float(ux - (ex << 23)), __int_as_float(uy - (ey << 23)));
-  const f2 l = mk2(__builtin_amdgcn_logf(m.x), __builtin_amdgcn_logf(m.y));
-  const f2 fe = mk2((float)ex, (float)ey);
-  const f2 p = y * fe;
-  const f2 pe = fma2(y, fe, -p);
-  const f2 q = y * l;
-  const f2 qe = fma2(y, l, -q);
-  const f2 ip = mk2(__builtin_rintf(p.x), __builtin_rintf(p.y));
-  const f2 f = ((p - ip) + q) + (pe + qe);
-  return mk2(__builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f.x), (int)ip.x),
-             __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(f.y), (int)ip.y));
-}
-
 // ---- lockstep forms: NP independent evaluations advanced one operation at a time, so a wave
 // carries NP dependency chains at once (the routing ticks are latency-bound at 4 waves/SIMD) ----
 #define DDR_FOR_NP _Pragma("unroll") for (int h = 0; h < NP; ++h)

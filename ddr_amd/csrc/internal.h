@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -58,16 +59,10 @@ __host__ __device__ inline int route_slot_stride(int max_slots) { return (max_sl
 // Forward x slots double-buffered by tick parity at KR <= 2 (one workgroup barrier per tick instead of
 // two: a tick's results go straight into the other buffer; the LDS is there at one or two reaches per
 // thread, not at four)
-#ifndef DDR_FWD_DBL
-#define DDR_FWD_DBL 1
-#endif
-__host__ __device__ constexpr int fwd_xbuf(int kr) { return (DDR_FWD_DBL && kr <= 2) ? 2 : 1; }
+__host__ __device__ constexpr int fwd_xbuf(int kr) { return kr <= 2 ? 2 : 1; }
 // The backward's three slot arrays (c1 gb, c2 gb, published x) likewise: each tick reads the values its
 // neighbours wrote the tick before and writes the next tick's, one barrier per tick (KR <= 2)
-#ifndef DDR_BWD_DBL
-#define DDR_BWD_DBL 1
-#endif
-__host__ __device__ constexpr int bwd_xbuf(int kr) { return (DDR_BWD_DBL && kr <= 2) ? 2 : 1; }
+__host__ __device__ constexpr int bwd_xbuf(int kr) { return kr <= 2 ? 2 : 1; }
 // reaches per thread of the routing kernels for a largest block of `max_load` reaches
 inline int kr_of_load(int64_t max_load) {
   int kr = 1;
@@ -198,6 +193,7 @@ struct Graph {
   bool device_built = false;  // built by build_graph_device: crow/col/down/... live in dviews only
   DeviceViews dviews;
   hipEvent_t ready = nullptr;  // device builds: recorded on the build stream once the schedule is complete
+  mutable std::atomic<bool> ready_waited{false};  // a launch outside a stream capture has waited for `ready`
   void* staging = nullptr;     // pinned host sources of the device build's last uploads
   std::vector<void*> allocations;        // hipMalloc (host builds)
   std::vector<void*> async_allocations;  // device_get blocks (device builds): returned stream-ordered
@@ -318,5 +314,6 @@ constexpr int kStatusNaN = 4;  // DDR_FWD_CHECK_QPRIME: a NaN in the flow-scaled
 constexpr int32_t kFlagForceTimeout = 1 << 16;  // debug: every inter-workgroup wait times out
 constexpr int32_t kFlagNoSteady = 1 << 17;      // debug / A/B: every tick through the general path
 constexpr int32_t kFlagNoStorer = 1 << 18;      // debug / A/B: light blocks store from their compute waves
+constexpr int32_t kFlagNoPlain = 1 << 19;       // debug / A/B: the general kernel instances, never the plain ones
 
 }  // namespace ddr

@@ -348,39 +348,6 @@ __device__ __forceinline__ PhysOut<float> coefficients_faithful(const ReachStati
   return o;
 }
 
-// coefficients_faithful of two reaches at once (packed halves): the same operations on the same values,
-// so the same bits; about two thirds of the issue slots of two scalar evaluations.
-__device__ __forceinline__ void coefficients_faithful2(const ReachStatic<float>& s0, const ReachStatic<float>& s1,
-                                                       float Q0, float Q1, const Consts<float>& c, PhysOut<float>& o0,
-                                                       PhysOut<float>& o1) {
-  auto cl2 = [](f2 x, float lo, float hi) { return mk2(rclamp(x.x, lo, hi), rclamp(x.y, lo, hi)); };
-  auto mx2 = [](f2 x, float lo) { return mk2(rmax(x.x, lo), rmax(x.y, lo)); };
-  const f2 n = mk2(s0.n, s1.n), qe = mk2(s0.qe, s1.qe), X = mk2(s0.X, s1.X);
-  const f2 ratio = div_rn2((mk2(Q0, Q1) * n) * (qe + sp2(1.0f)), mk2(s0.dd, s1.dd));
-  const f2 depth = mx2(pow_faithful2(ratio, mk2(s0.expo, s1.expo)), c.dlb);
-  const f2 dq = pow_faithful2(depth, qe);
-  const f2 tw = mk2(s0.p, s1.p) * dq;
-  const f2 ssr = div_rn2(tw * qe, sp2(2.0f) * depth);
-  const f2 ss = cl2(ssr, c.sslb, c.ssub);
-  const f2 bw = mx2(tw - (sp2(2.0f) * ss) * depth, c.bwlb);
-  const f2 area = ((tw + bw) * depth) * sp2(0.5f);
-  const f2 u = sp2(1.0f) + ss * ss;
-  const f2 wp = bw + (sp2(2.0f) * depth) * mk2(sqrt_rn_normal(u.x), sqrt_rn_normal(u.y));
-  const f2 Rh = div_rn2(area, wp);
-  const f2 r23 = pow_faithful2(Rh, sp2(two_thirds<float>()));
-  const f2 cel = div_rn2(cl2((mk2(s0.inv_n, s1.inv_n) * r23) * mk2(s0.sqrtS, s1.sqrtS), c.vlb, c.vub) * sp2(5.0f),
-                         sp2(3.0f));
-  const f2 twok = sp2(2.0f) * div_rn2(mk2(s0.L, s1.L), cel);
-  const f2 omX = sp2(1.0f) - X;
-  const f2 den = (twok * omX) + sp2(c.dt);
-  const f2 c1 = div_rn2(sp2(c.dt) - twok * X, den);
-  const f2 c2 = div_rn2(sp2(c.dt) + twok * X, den);
-  const f2 c3 = div_rn2((twok * omX) - sp2(c.dt), den);
-  const f2 c4 = div_rn2(sp2(2.0f * c.dt), den);
-  o0.c1 = c1.x; o0.c2 = c2.x; o0.c3 = c3.x; o0.c4 = c4.x; o0.tw = tw.x; o0.ss = ss.x;
-  o1.c1 = c1.y; o1.c2 = c2.y; o1.c3 = c3.y; o1.c4 = c4.y; o1.tw = tw.y; o1.ss = ss.y;
-}
-
 // VJP of (c1, c2, c3, c4) w.r.t. (Q, n, q_spatial, p_spatial) at the point described by g.
 template <typename R, bool Fast = false>
 __device__ __forceinline__ void coefficients_vjp(const ReachStatic<R>& s, R Q, const Consts<R>& c,
@@ -547,101 +514,6 @@ __device__ __forceinline__ AdjOut adjoint_step_fast(const ReachStatic<float>& s,
   o.gq = g_qe;
   o.gp = g_p;
   return o;
-}
-
-// adjoint_step_fast of two reaches at once (packed halves; the same operations, so the same bits).
-struct AdjIn {
-  float Q, gb, a1, a2, a3;  // adjoint_step_fast's
-};
-template <bool DF>
-__device__ __forceinline__ void adjoint_step_fast2(const ReachStatic<float>& s0, const ReachStatic<float>& s1,
-                                                   const AdjIn& i0, const AdjIn& i1, const Consts<float>& c, AdjOut& o0,
-                                                   AdjOut& o1) {
-  constexpr float kLn2 = 0.69314718055994530942f;
-  auto pr = [](float a, float b) { return mk2(a, b); };
-  auto rcp = [](f2 a) { return mk2(__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)); };
-  auto lg = [](f2 a) { return mk2(__builtin_amdgcn_logf(a.x), __builtin_amdgcn_logf(a.y)); };
-  auto ex = [](f2 a) { return mk2(__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)); };
-  auto mx = [](f2 a, float lo) { return mk2(rmax(a.x, lo), rmax(a.y, lo)); };
-  auto cl = [](f2 a, float lo, float hi) { return mk2(rclamp(a.x, lo, hi), rclamp(a.y, lo, hi)); };
-  const f2 Q = pr(i0.Q, i1.Q), gb = pr(i0.gb, i1.gb), U = pr(i0.a1, i1.a1), V = pr(i0.a2, i1.a2), W = pr(i0.a3, i1.a3);
-  const f2 qe = pr(s0.qe, s1.qe), qe1 = qe + sp2(1.0f), expo = pr(s0.expo, s1.expo);
-  const f2 n = pr(s0.n, s1.n), p = pr(s0.p, s1.p), inv_n = pr(s0.inv_n, s1.inv_n), sqrtS = pr(s0.sqrtS, s1.sqrtS);
-  const f2 L = pr(s0.L, s1.L), X = pr(s0.X, s1.X);
-  // ---- recompute ----
-  const f2 num = (Q * n) * qe1;
-  const f2 rdd = rcp(pr(s0.dd, s1.dd));
-  const f2 ratio = num * rdd;
-  const f2 l2r = lg(ratio);
-  const f2 pw = ex(expo * l2r);
-  const f2 depth = mx(pw, c.dlb);
-  const f2 l2d = lg(depth);
-  const f2 dq = ex(qe * l2d);
-  const f2 tw = p * dq;
-  const f2 td = depth + depth;
-  const f2 rtd = rcp(td);
-  const f2 ssr = (tw * qe) * rtd;
-  const f2 ss = cl(ssr, c.sslb, c.ssub);
-  const f2 bwr = tw - (ss + ss) * depth;
-  const f2 bw = mx(bwr, c.bwlb);
-  const f2 area = ((tw + bw) * depth) * sp2(0.5f);
-  const f2 u = fma2(ss, ss, sp2(1.0f));
-  const f2 isq = mk2(__builtin_amdgcn_rsqf(u.x), __builtin_amdgcn_rsqf(u.y));
-  const f2 sq = u * isq;
-  const f2 wp = fma2(td, sq, bw);
-  const f2 rwp = rcp(wp);
-  const f2 Rh = area * rwp;
-  const f2 r23 = ex(lg(Rh) * sp2(2.0f / 3.0f));
-  const f2 v = (inv_n * r23) * sqrtS;
-  const f2 cel = cl(v, c.vlb, c.vub) * sp2(5.0f / 3.0f);
-  const f2 rcel = rcp(cel);
-  const f2 twok = sp2(2.0f) * (L * rcel);
-  const f2 omX = sp2(1.0f) - X;
-  const f2 den = fma2(twok, omX, sp2(c.dt));
-  const f2 rden = rcp(den);
-  const f2 tX = twok * X;
-  const f2 c1 = (sp2(c.dt) - tX) * rden;
-  const f2 c2 = (sp2(c.dt) + tX) * rden;
-  const f2 c4 = sp2(2.0f * c.dt) * rden;
-  const f2 c3 = sp2(1.0f) - c4;
-  // ---- VJP ----
-  const f2 g_twok = DF ? (gb * fma2(U, fma2(omX, c1, X), V * fma2(omX, c2, -X))) * rden
-                       : gb * fma2(X, W - V, omX * (Q - U)) * rden;
-  const f2 g_cel = -(g_twok * twok) * rcel;
-  const f2 gvc = (g_cel * sp2(5.0f / 3.0f)) * v;
-  const f2 gvv = mk2((v.x >= c.vlb && v.x <= c.vub) ? gvc.x : 0.0f, (v.y >= c.vlb && v.y <= c.vub) ? gvc.y : 0.0f);
-  f2 g_n = -gvv * inv_n;
-  const f2 G = gvv * sp2(2.0f / 3.0f);
-  const f2 g_area = G * rcp(area);
-  const f2 g_wp = -G * rwp;
-  const f2 ha = (g_area * depth) * sp2(0.5f);
-  f2 g_bw = g_wp + ha;
-  f2 g_tw = ha;
-  f2 g_depth = fma2(sp2(2.0f) * sq, g_wp, (G + G) * rtd);
-  f2 g_ss = ((td * g_wp) * ss) * isq;
-  const f2 g_bwr = mk2(bwr.x >= c.bwlb ? g_bw.x : 0.0f, bwr.y >= c.bwlb ? g_bw.y : 0.0f);
-  g_tw += g_bwr;
-  g_ss = fma2(-td, g_bwr, g_ss);
-  g_depth = fma2(-(ss + ss), g_bwr, g_depth);
-  const f2 g_ssr = mk2((ssr.x >= c.sslb && ssr.x <= c.ssub) ? g_ss.x : 0.0f,
-                       (ssr.y >= c.sslb && ssr.y <= c.ssub) ? g_ss.y : 0.0f);
-  const f2 gsr = g_ssr * rtd;
-  g_tw = fma2(gsr, qe, g_tw);
-  f2 g_qe = gsr * tw;
-  g_depth = fma2(-(g_ssr + g_ssr) * ssr, rtd, g_depth);
-  f2 g_p = g_tw * dq;
-  const f2 gtt = g_tw * tw;
-  g_depth = fma2((gtt + gtt) * qe, rtd, g_depth);
-  g_qe = fma2(gtt * sp2(kLn2), l2d, g_qe);
-  const f2 g_pw = mk2(pw.x >= c.dlb ? g_depth.x : 0.0f, pw.y >= c.dlb ? g_depth.y : 0.0f);
-  const f2 A = (g_pw * expo) * pw;
-  g_qe = fma2(-((g_pw * pw) * (l2r * sp2(kLn2))), expo * expo, g_qe);
-  const f2 gQ = A * rcp(Q);
-  g_n = fma2(A, inv_n, g_n);
-  g_qe = fma2(A, rcp(qe1), g_qe);
-  g_p = fma2(-A * sqrtS, rdd, g_p);
-  o0.c1 = c1.x; o0.c2 = c2.x; o0.c3 = c3.x; o0.c4 = c4.x; o0.gQ = gQ.x; o0.gn = g_n.x; o0.gq = g_qe.x; o0.gp = g_p.x;
-  o1.c1 = c1.y; o1.c2 = c2.y; o1.c3 = c3.y; o1.c4 = c4.y; o1.gQ = gQ.y; o1.gn = g_n.y; o1.gq = g_qe.y; o1.gp = g_p.y;
 }
 
 }  // namespace ddr

@@ -14,6 +14,8 @@
 // pre-activations Z1..Z3 (3 x N x 128) and the sigmoid U (N x 3) for the backward; the backward accumulates
 // its weight gradients in registers over its tiles and writes one partial per workgroup, summed in a fixed
 // order by pnet_reduce_kernel (deterministic).
+#include <atomic>
+
 #include "internal.h"
 
 namespace ddr {
@@ -451,12 +453,21 @@ __global__ void pnet_reduce_kernel(const float* partial, int nwg, int total, flo
   grad[p] = v;
 }
 
-int pnet_grid(int64_t ntiles) {
-  int dev = 0, cus = 256;
-  hipDeviceProp_t prop;
-  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, cus));
+// CUs of the current device, queried once per device (three calls per training step: no device-properties
+// query on the host's critical path)
+int device_cus() {
+  constexpr int kDevs = 64;
+  static std::atomic<int> cache[kDevs] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevs) return 256;
+  int cus = cache[dev].load(std::memory_order_relaxed);
+  if (cus == 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    cache[dev].store(cus, std::memory_order_relaxed);
+  }
+  return cus;
 }
+int pnet_grid(int64_t ntiles) { return (int)std::max<int64_t>(1, std::min<int64_t>(ntiles, device_cus())); }
 
 }  // namespace
 

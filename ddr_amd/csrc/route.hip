@@ -33,37 +33,20 @@
 
 namespace ddr {
 
-// experiments: the fp32 adjoint's recompute in the exact operation set (profiles/r02: no accuracy gain)
-#ifndef DDR_BWD_EXACT
-#define DDR_BWD_EXACT 0
-#endif
-#ifndef DDR_BWD_EARLY_LOADS
-#define DDR_BWD_EARLY_LOADS 1
-#endif
-// Skip the physics of a wave-slice none of whose lanes runs a step in this tick.  Forward: C3 -7 %,
-// C5 -2 %, route_timestep 9.2 -> 3.5 ms at 800k; backward: no gain measured (+0.8 % C5), off
-// (profiles/r02/ab_defer_early.txt)
-#ifndef DDR_SKIP_IDLE
-#define DDR_SKIP_IDLE 1
-#endif
-#ifndef DDR_SKIP_IDLE_BWD
-#define DDR_SKIP_IDLE_BWD 0
-#endif
-#ifndef DDR_BWD_STEADY
-#define DDR_BWD_STEADY 1
-#endif
-#ifndef DDR_BWD_EARLY_MAX_KR
-#define DDR_BWD_EARLY_MAX_KR 2  // KR = 4 has no registers for the second set (spills)
-#endif
-// The KR = 4 backward's steady ticks without the dL/drunoff group clamps, and its group select as two bit tests
-// and three selects instead of a ternary chain the compiler turned into divergent branches: C5 backward
-// 57.3 -> 53.9 ms (profiles/r05/ab_r05.txt item 10); the same loaded values, the same bits
-#ifndef DDR_BWD_GRAD_NOCLAMP
-#define DDR_BWD_GRAD_NOCLAMP 1
-#endif
-#ifndef DDR_BWD_SEL_BITS
-#define DDR_BWD_SEL_BITS 1
-#endif
+// Tuning constants (each chosen by an A/B on MI355X; the rejected alternatives live in git history and
+// profiles/r0*/ab_*.txt, not here):
+// The backward's early loads (the next tick's x(t - 3) and virtual x requested at the top of the tick into a
+// second register set) and its double-buffered slots at KR <= 2; KR = 4 has no registers for the second set
+constexpr int kBwdEarlyMaxKR = 2;
+// The backward's dL/drunoff groups as shift registers at KR <= 2 (c3s8 backward -4 %); at KR = 4 a select on
+// t & 3 as two bit tests and three selects (C5 backward 59.5 vs 57.3 ms, profiles/r05/ab_r05.txt)
+constexpr int kBwdShiftMaxKR = 2;
+// Import waves: a chunk's cut-out granules requested this many ticks before its boundary tick
+constexpr int kBwdImpEarly = 4;
+// x / gradient helpers: their loads issued this many ticks ahead
+constexpr int kBwdHelpAhead = 3;
+// The clamps' infinity opaque to the compiler from this KR on (one v_med3_f32 per clamp)
+constexpr int kOpqInfMinKR = 4;
 
 namespace {
 
@@ -76,24 +59,17 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Wave priority by remaining slices (DDR_SLICE_PRIO): the SIMD's arbiter serves its oldest ready wave
+// Wave priority by remaining slices: the SIMD's arbiter serves its oldest ready wave
 // first, so the workgroup's first waves finish their slices early and the youngest runs its last slices
 // alone at the end of every tick, one dependent chain issuing on the SIMD.  A wave at slice k of KR takes
 // priority KR - 1 - k (the top of the tick: 3), so the waves with more work left go first and the
 // SIMD's waves finish together.  KR = 4 (full load): C5 129.4 -> 126.2 ms, C3 forward 16.0 -> 14.4 ms
 // (profiles/r04/ab_r04.txt item 28); at KR = 2 no gain was measured (C4), KR = 1 has one slice.
-#ifndef DDR_SLICE_PRIO
-#define DDR_SLICE_PRIO 1
-#endif
-// (DDR_LIGHT_PRIO, forward at KR = 1) a routing wave runs its step's physics at priority 1 and the rest at 0:
+// (forward at KR = 1) a routing wave runs its step's physics at priority 1 and the rest at 0:
 // of the two routing waves on a SIMD, the one ahead yields once its physics is done, so the two finish
 // together (c3s8 forward 2.87 -> 2.75 ms; C2 and c5s8r5 within noise; the backward's adjoint showed no
 // change; profiles/r04/ab_r04.txt item 30)
-#ifndef DDR_LIGHT_PRIO
-#define DDR_LIGHT_PRIO 1
-#endif
 __device__ __forceinline__ void set_prio(int p) {
-  if (!DDR_SLICE_PRIO) return;
   switch (p) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
     case 1: __builtin_amdgcn_s_setprio(1); break;
@@ -263,18 +239,12 @@ constexpr unsigned kWaitVmcnt0 = 0x0F70;
 // Kernel-argument constants in R (pre-rounded on the host, so they stay scalar operands).
 // pin_pow: keep the fp64 constants of the correctly rounded pow in VGPRs (kernels that evaluate it).
 // opq_inf: the clamps' infinity opaque to the compiler (rmaxc: one v_med3_f32 per clamp; the KR = 4 kernels)
-#ifndef DDR_OPQ_INF_MIN_KR
-#define DDR_OPQ_INF_MIN_KR 4
-#endif
 template <typename R>
 __device__ __forceinline__ Consts<R> consts_of(const RouteArgs& a, bool pin_pow = true, bool opq_inf = false);
 template <>
 __device__ __forceinline__ Consts<float> consts_of<float>(const RouteArgs& a, bool pin_pow, bool opq_inf) {
-#ifndef DDR_PIN_POWK
-#define DDR_PIN_POWK 1
-#endif
   return Consts<float>{a.cf[0], a.cf[1], a.cf[2], a.cf[3], a.cf[4], a.cf[5], a.cf[6], a.cf[7],
-                       (DDR_PIN_POWK && pin_pow) ? pow_consts_vgpr() : pow_consts(), a.ln_dlb,
+                       pin_pow ? pow_consts_vgpr() : pow_consts(), a.ln_dlb,
                        opq_inf ? opaque_inf(__builtin_inff()) : __builtin_inff()};
 }
 template <>
@@ -318,30 +288,11 @@ __device__ __forceinline__ V opq(V x) {
 }
 __device__ __forceinline__ int up_n(unsigned u) { return (int)(u >> 26); }
 // 16-B runoff row segments (plain stores: measured faster than 8-B segments and than nt stores)
-#ifndef DDR_RUNOFF_NT
-#define DDR_RUNOFF_NT 0
-#endif
 __device__ __forceinline__ void store4(float* p, float a, float b, float c, float d) {
-  if (DDR_RUNOFF_NT) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = {a, b, c, d};
-    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(p));
-    return;
-  }
   *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
 }
-#ifndef DDR_GRAD_NT
-#define DDR_GRAD_NT 0
-#endif
-// a dL/drunoff group (streamed: each 16-B piece of a row is read once per launch)
-__device__ __forceinline__ float4 load_grad4(const float* p) {
-  if (DDR_GRAD_NT) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-  }
-  return *reinterpret_cast<const float4*>(p);
-}
+// a dL/drunoff group (each 16-B piece of a row is read once per launch; plain loads: nt measured slower)
+__device__ __forceinline__ float4 load_grad4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void store4(double* p, double a, double b, double c, double d) {
   reinterpret_cast<double2*>(p)[0] = make_double2(a, b);
   reinterpret_cast<double2*>(p)[1] = make_double2(c, d);
@@ -466,12 +417,6 @@ __device__ __forceinline__ const R* qs_at(const RouteArgs& a, const BlockDesc& B
 //            physics and the fp64 column sweep, keeps x in a register          -- barrier --
 //   publish: x into the reach's own slot (and virtual inflows into theirs)      -- barrier --
 // The inflow I(t+1) = sum_j Q_j(t) is formed from the same x_j(t) reads (Q_j = clamp(x_j)).
-#ifndef DDR_FWD_TOPWAIT
-#define DDR_FWD_TOPWAIT 1
-#endif
-#ifndef DDR_FWD_UNROLL2
-#define DDR_FWD_UNROLL2 1
-#endif
 // FM (fp32 only, DDR_FWD_FAST_MATH): the coefficients in hardware-approximate fp32 math
 // (coefficients_fast, the operation set of the adjoint's recompute) instead of the reference's exact
 // operation sequence; ~1e-6 relative per coefficient, and few enough registers that all of a
@@ -488,20 +433,11 @@ __device__ __forceinline__ const R* qs_at(const RouteArgs& a, const BlockDesc& B
 template <typename R, int KR, int MATH, int XB = 0, int PL = 0>
 __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 256) route_forward_kernel(RouteArgs a) {
   constexpr int BS = kBlockThreads;
-#ifndef DDR_FWD_NP
-#define DDR_FWD_NP 1
-#endif
-#ifndef DDR_FWD_NP_FAST
-#define DDR_FWD_NP_FAST 1
-#endif
-  // faithful: slice pairs in packed halves (coefficients_faithful2)
-#ifndef DDR_FWD_NP_FAITH
-#define DDR_FWD_NP_FAITH 1
-#endif
   constexpr bool kFast = MATH == 1 && std::is_same<R, float>::value;
   constexpr bool kFaith = MATH == 2 && std::is_same<R, float>::value;
-  constexpr int NPW = kFast ? DDR_FWD_NP_FAST : (kFaith ? DDR_FWD_NP_FAITH : DDR_FWD_NP);
-  constexpr int NP = KR < NPW ? KR : NPW;  // slices whose physics runs in lockstep
+  // one slice's physics at a time (lockstep slice pairs, plain or in packed halves, measured slower:
+  // DESIGN section 4)
+  constexpr int NP = 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int bid = take_ticket(a.status, kStatusTicketFwd, a.nblocks, false, reinterpret_cast<int*>(smem));
   if (a.owned && !a.owned[bid]) return;  // split basin: another rank's block
@@ -520,7 +456,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const StatTab<R> tab{reinterpret_cast<R*>(sx + kXBuf * S)};           // [S][6]
   double* ring = reinterpret_cast<double*>(smem + kMathTabBytes + align16(size_t(S) * (8 * kXBuf + 6 * sizeof(R))));  // [nvirt][kChunkFwd]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                     // confluence lists
-  const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith, KR >= DDR_OPQ_INF_MIN_KR);
+  const Consts<R> cs = consts_of<R>(a, !kFast && !kFaith, KR >= kOpqInfMinKR);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool accum = !PL && (a.flags & DDR_FWD_ACCUMULATE);  // every step a hot start (daily accumulation)
@@ -551,26 +487,17 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // Storer waves (one reach per thread, blocks of at most half a workgroup): the idle upper half of the
   // workgroup stores each reach's published x (x_save row, runoff) during the next tick, so a compute
   // wave's top-of-tick wait covers only its q' prefetch -- not the acknowledgement of its stores, which
-  // is on a light block's critical path (up to 12 % of a C2 tick, profiles/r03/ab_r03.txt item 5)
-#ifndef DDR_FWD_STORER
-#define DDR_FWD_STORER 1
-#endif
-  // imports requested a chunk ahead (KR <= 2: registers for the chunk's raw granules)
-#ifndef DDR_FWD_PREF_IMPORT
-#define DDR_FWD_PREF_IMPORT 1
-#endif
-  constexpr bool kPrefImport = DDR_FWD_PREF_IMPORT && KR <= 2;
+  // is on a light block's critical path (up to 12 % of a C2 tick, profiles/r03/ab_r03.txt item 5).
+  // The storers export the cut reaches' granules too: a cut reach's x reaches its consumer one tick later
+  // (pipeline latency of that hand-off only), and no compute wave waits for a store at all.
+  // Imports requested a chunk ahead (KR <= 2: registers for the chunk's raw granules).
+  constexpr bool kPrefImport = KR <= 2;
   unsigned long long pfg[kChunkFwd];
 #pragma unroll
   for (int i = 0; i < kChunkFwd; ++i) pfg[i] = 0ull;
-  const bool storer_mode = KR == 1 && DDR_FWD_STORER && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2;
+  const bool storer_mode = KR == 1 && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2;
   const bool storer_wave = storer_mode && wbase >= BS / 2;
   const int sr = tid - BS / 2;  // a storer thread's reach
-  // storer-side granule exports too (DDR_FWD_STORER_GRANULES): a cut reach's x reaches its consumer one
-  // tick later (pipeline latency of that hand-off only), and no compute wave waits for a store at all
-#ifndef DDR_FWD_STORER_GRANULES
-#define DDR_FWD_STORER_GRANULES 1
-#endif
   int sref = 0, soff = 0;  // soff: tick offset | 1 + cut rank << 16, as off[]
   if (storer_wave && sr < B.nloc) {
     sref = a.s.ref[B.pos0 + sr];
@@ -597,14 +524,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   }
   if (tid == 0) sx[S - 1] = 0.0;
   if (kDbl && tid == 0) sx[2 * S - 1] = 0.0;
-#ifndef DDR_FWD_VOWN_HIGH
-#define DDR_FWD_VOWN_HIGH 1
-#endif
   // virtual inflow vi is imported and published by thread BS - 1 - vi: the owners sit in the last
   // waves, which hold fewer wave-slices than wave 0 when nloc is not a multiple of 1024 (the import's
   // global round trip lands on the lighter waves; only the owner reads its ring entries, so the import
   // needs no workgroup barrier)
-  const int vi = DDR_FWD_VOWN_HIGH ? BS - 1 - tid : tid;
+  const int vi = BS - 1 - tid;
   const bool vown = vi < B.nvirt;
   int v_off = 0, v_edge = 0;
   if (vown) {
@@ -658,7 +582,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if (t < 0 || t >= T) return;
     const double xd = sx[(kDbl ? (taup & 1) * S : 0) + sr];
     const R xr = R(xd);
-    if (DDR_FWD_STORER_GRANULES && B.ncout > 0 && (so >> 16)) {
+    if (B.ncout > 0 && (so >> 16)) {
       const int64_t e = B.cout0 + (so >> 16) - 1;
       if (xt_off) {
         const uintptr_t p = xt[(so >> 16) - 1];
@@ -730,10 +654,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
           }
         }
       }
-#ifndef DDR_FWD_IMPORT_BARRIER
-#define DDR_FWD_IMPORT_BARRIER 0
-#endif
-      if (DDR_FWD_IMPORT_BARRIER) lds_barrier();
       if (aprof) prof_wait += __builtin_amdgcn_s_memrealtime() - w0;
     }
   };
@@ -748,14 +668,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // One tick of the waves that route reaches (every wave outside storer mode)
   auto tick = [&](int tau, R(&qcur)[KR], R(&qnext)[KR], auto sc) {
     constexpr bool kSt = decltype(sc)::value;
-#if DDR_FWD_TOPWAIT
     // the previous tick's q' prefetch and stores land here (see the backward kernel's tick); unconditional,
     // so the compiler's own wait analysis sees no load outstanding past it (a wait it could not prove made
     // it wait again, vmcnt(0), at the first use of qcur -- after this tick's prefetch was issued)
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-#endif
     if constexpr (KR == 4) set_prio(3);
-    if constexpr (KR == 1 && DDR_LIGHT_PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (KR == 1) __builtin_amdgcn_s_setprio(1);
     phz.mark(0);  // the previous tick's loads and stores
     // opaque per tick: everything derived from them (LDS / global offsets, masks) is recomputed
     // instead of being hoisted into registers held across the loop
@@ -782,7 +700,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     for (int k0 = 0; k0 < KR; k0 += NP) {
       if (wbase + k0 * BS >= B.nloc) continue;
       if constexpr (KR == 4) set_prio(KR - 1 - k0);
-      if (!kSt && DDR_SKIP_IDLE) {
+      if (!kSt) {
         // no lane of the wave runs a step this tick (before its first / after its last step: the
         // first and last dmax ticks of a block, most ticks of a short window): skip the slice
         bool act = false;
@@ -816,13 +734,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
           for (int h = 0; h < NP; ++h) ph[h] = coefficients_fast(st[h], Qv[h], cs);
         } else if constexpr (kFaith) {
-          if constexpr (NP == 2) {
-            // the pair's physics in packed halves (the same bits as two scalar evaluations)
-            coefficients_faithful2(st[0], st[1], Qv[0], Qv[1], cs, ph[0], ph[1]);
-          } else {
 #pragma unroll
-            for (int h = 0; h < NP; ++h) ph[h] = coefficients_faithful(st[h], Qv[h], cs);
-          }
+          for (int h = 0; h < NP; ++h) ph[h] = coefficients_faithful(st[h], Qv[h], cs);
         } else {
           coefficients_np<R, NP>(st, Qv, cs, ph);
         }
@@ -830,7 +743,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
 #pragma unroll
         for (int h = 0; h < NP; ++h) ph[h] = PhysOut<R>{R(0), R(0), R(0), R(0), R(0), R(0)};
       }
-      if constexpr (KR == 1 && DDR_LIGHT_PRIO) __builtin_amdgcn_s_setprio(0);
+      if constexpr (KR == 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int h = 0; h < NP; ++h) {
         const int k = k0 + h;
@@ -879,10 +792,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if (hk && (kSt || (t >= 0 && t < T))) {
           const R xr = R(x);
           const R Qn = raw ? xr : rmax_nan(xr, cs.qlb);
-#ifndef DDR_EXP_NO_FWD_STORES
-#define DDR_EXP_NO_FWD_STORES 0  // timing experiment only: no x_save / runoff stores (wrong results)
-#endif
-          const bool own_st = !DDR_EXP_NO_FWD_STORES && !storer_mode;  // (storer mode: the upper waves store)
+          const bool own_st = !storer_mode;  // (storer mode: the upper waves store)
           if (own_st) xrow[r] = xr;  // the routing state for the adjoint
           if (emit && own_st) {
             // runoff[ref, t] = max(x(t), qlb)  (mmc.py:412 for t = 0, mmc.py:557 after every step)
@@ -891,15 +801,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
             ob2[k] = ob3[k];
             ob3[k] = rmax_nan(xr, cs.qlb);
             R* orow = runoff + (int64_t)ref[k] * T;
-#ifndef DDR_EXP_RUNOFF_DUMMY
-#define DDR_EXP_RUNOFF_DUMMY 0  // timing experiment only: runoff stores into a 256-KB window (wrong results)
-#endif
-            if (DDR_EXP_RUNOFF_DUMMY) {
-              if ((t & 3) == 3) store4(runoff + ((int64_t)(ref[k] & 1023) << 6) + ((t - 3) & 60), ob0[k], ob1[k], ob2[k], ob3[k]);
-            } else if (!emit4) orow[t] = ob3[k];
+            if (!emit4) orow[t] = ob3[k];
             else if ((t & 3) == 3) store4(orow + (t - 3), ob0[k], ob1[k], ob2[k], ob3[k]);
           }
-          if (B.ncout > 0 && (off[k] >> 16) && !(DDR_FWD_STORER_GRANULES && storer_mode)) {
+          if (B.ncout > 0 && (off[k] >> 16) && !storer_mode) {
             const int64_t e = B.cout0 + (off[k] >> 16) - 1;
             if (xt_off) {  // split basin: the row from the block's table (another rank's: system scope)
               const uintptr_t p = xt[(off[k] >> 16) - 1];
@@ -969,16 +874,12 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   using Gen = std::integral_constant<bool, false>;
   using Steady = std::integral_constant<bool, true>;
   prefetch(0, qa, tid, Gen{});
-#if DDR_FWD_UNROLL2
   // two ticks per iteration, the prefetch registers swapping roles: copying the prefetched q'
   // (qa = qb) at the loop latch would wait for the loads just issued, and for every store of the tick.
   // Steady ticks [s0, s1) (even bounds, so the roles keep alternating) between the ramps.
-#ifndef DDR_FWD_STEADY
-#define DDR_FWD_STEADY 1
-#endif
   int s0 = B.dmax + 1, s1 = (int)T & ~1;
   s0 += s0 & 1;
-  if (!DDR_FWD_STEADY || (a.flags & kFlagNoSteady) || accum || s1 <= s0) s0 = s1 = 0;
+  if ((a.flags & kFlagNoSteady) || accum || s1 <= s0) s0 = s1 = 0;
 #pragma unroll 1
   for (int tau = 0; tau < s0; tau += 2) {
     if (aprof && tid == 0) prof_tick(aprof, bid, tau);
@@ -997,16 +898,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     tick(tau, qa, qb, Gen{});
     if (tau + 1 < TT) tick(tau + 1, qb, qa, Gen{});
   }
-#else
-  // not unrolled: one copy of the tick body keeps the loop inside the instruction cache
-#pragma unroll 1
-  for (int tau = 0; tau < TT; ++tau) {
-    if (aprof && tid == 0) prof_tick(aprof, bid, tau);
-    tick(tau, qa, qb, Gen{});
-#pragma unroll
-    for (int k = 0; k < KR; ++k) qa[k] = qb[k];
-  }
-#endif
   if (aprof && tid == 0) prof_end(aprof, bid, prof_wait);
   phz.flush(aprof, a.nblocks, bid);
 }
@@ -1143,14 +1034,14 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // and writes its own for the next tick into the other buffers: one workgroup barrier per tick.  Else
   // [S] each, a publish phase and a compute phase between two barriers.
   constexpr int kXB = XB > 0 ? XB : bwd_xbuf(KR);
-  constexpr bool kDbl = kXB == 2 && (DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR);
+  constexpr bool kDbl = kXB == 2 && KR <= kBwdEarlyMaxKR;
   R* sa = reinterpret_cast<R*>(smem + kMathTabBytes);  // [kXB][S] c1_i gb_i (transposed solve, rounded to R)
   R* sb = sa + kXB * S;                                 // [kXB][S] c2_i gb_i (adjoint of the inflow)
   R* sx = sb + kXB * S;                                 // [kXB][S] x(t - 2) of each reach / virtual inflow; [S-1] = 0
   const StatTab<R> tab{sx + kXB * S};                   // [S][6]
   R* ring = reinterpret_cast<R*>(smem + kMathTabBytes + align16(size_t(S) * (3 * kXB + 6) * sizeof(R)));  // [ncout][kChunkBwd][2]
   int* xl = reinterpret_cast<int*>(smem + a.xl_off);                                            // confluence lists
-  const Consts<R> cs = consts_of<R>(a, true, KR >= DDR_OPQ_INF_MIN_KR);
+  const Consts<R> cs = consts_of<R>(a, true, KR >= kOpqInfMinKR);
   const int64_t T = a.T;
   const bool carry = a.flags & DDR_FWD_CARRY;
   const bool force_to = a.flags & kFlagForceTimeout;
@@ -1184,41 +1075,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   // kDF (DDR_BWD_EXACT_ADJOINT, fp32 fast adjoint): the step's mass imbalances D1 = Q - qc - Sx, D2 = Q - qc - I
   // formed in fp64 from the fp32 states (physics.h adjoint_step_fast): the upstream sums carried in fp64, qc
   // re-read.  Else X (I - Sx) + (1 - X)(Q - x~) with x~ := x(t), the stored state
-  constexpr bool kDF = DF && std::is_same<R, float>::value && !DDR_BWD_EXACT;
-#ifndef DDR_EXP_DF_F32
-#define DDR_EXP_DF_F32 0
-#endif
-#ifndef DDR_EXP_DF_NOQ
-#define DDR_EXP_DF_NOQ 0
-#endif
-  using SxT = typename std::conditional<kDF && !DDR_EXP_DF_F32, double, R>::type;
+  constexpr bool kDF = DF && std::is_same<R, float>::value;
+  using SxT = typename std::conditional<kDF, double, R>::type;
   SxT sxn[KR];
   // the gradient groups as shift registers (KR <= 2: c3s8 backward -4 %); at KR = 4 the select on t & 3 measured
   // faster (C5 backward 59.5 vs 57.3 ms, profiles/r05/ab_r05.txt)
-#ifndef DDR_BWD_SHIFT_MAX_KR
-#define DDR_BWD_SHIFT_MAX_KR 2
-#endif
-  constexpr bool kShiftG = KR <= DDR_BWD_SHIFT_MAX_KR;
-  // early loads (DDR_BWD_EARLY_LOADS): the next tick's x(t - 3) and virtual x are requested at the top
+  constexpr bool kShiftG = KR <= kBwdShiftMaxKR;
+  // early loads: the next tick's x(t - 3) and virtual x are requested at the top
   // of the tick into a second register set (roles swap every tick: the loop is unrolled by two), so
   // they have the whole tick to land instead of the part after the first barrier
   R xb2[KR];
-  constexpr bool kEarly = DDR_BWD_EARLY_LOADS && KR <= DDR_BWD_EARLY_MAX_KR;
+  constexpr bool kEarly = KR <= kBwdEarlyMaxKR;
   // gauge mode, KR <= 2: each reach's gauge when it has exactly one (else -1: none, or several -- the
   // reach -> gauge list is walked), so the tick's dL/dout loads are one address computation, not a chain of
   // three dependent loads each followed by a wait
   constexpr bool kGReg = KR <= 2;
   int gsg[kGReg ? KR : 1];
-  constexpr bool kQs = GS || (kDF && !DDR_EXP_DF_NOQ);
+  constexpr bool kQs = GS || kDF;
   R qsv[kQs ? KR : 1];  // q' * flow_scale of this tick's step (prefetched a tick ahead): state gradients, kDF
   // one reach per thread: the derived statics stay in registers (see the forward)
   constexpr bool kStatReg = KR == 1 && sizeof(R) == 4;
   ReachStatic<R> sreg[kStatReg ? KR : 1];
-  // slice pairs whose adjoint steps run in packed halves (fp32 adjoint, KR >= 2)
-#ifndef DDR_BWD_PAIR
-#define DDR_BWD_PAIR 0
-#endif
-  constexpr int NPB = (DDR_BWD_PAIR && KR >= 2 && std::is_same<R, float>::value && !DDR_BWD_EXACT) ? 2 : 1;
 #pragma unroll
   for (int k = 0; k < KR; ++k) {
     const int r = tid + k * BS;
@@ -1241,7 +1118,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     if constexpr (kStatReg) {
       const ReachStatic<R> ls = load_static<R>(a, ref[k]);
       // the LDS path derives the same fields with the same operations each tick (StatTab::get)
-      sreg[k] = derive_static<R, !DDR_BWD_EXACT>(ls.n, ls.qe, ls.p, ls.sqrtS, ls.L, ls.X);
+      sreg[k] = derive_static<R, true>(ls.n, ls.qe, ls.p, ls.sqrtS, ls.L, ls.X);
     }
   }
   for (int c = 0; c < B.ncout; ++c) {
@@ -1255,37 +1132,22 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
   const bool vown = tid < B.nvirt;
   // Import waves (KR = 1, blocks whose reaches, virtuals and chunk imports each fit half the workgroup):
   // the upper half's idle waves run the cut-out imports in a loop of their own, requesting each chunk's
-  // granules DDR_BWD_IMP_EARLY ticks before its boundary tick, so the routing waves' import phase shrinks
+  // granules kBwdImpEarly ticks before its boundary tick, so the routing waves' import phase shrinks
   // to the barrier that hands the ring over
-#ifndef DDR_BWD_IMPWAVES
-#define DDR_BWD_IMPWAVES 1
-#endif
-#ifndef DDR_BWD_IMP_EARLY
-#define DDR_BWD_IMP_EARLY 4
-#endif
-  static_assert(DDR_BWD_IMP_EARLY >= 0 && DDR_BWD_IMP_EARLY < kChunkBwd, "import lead within a chunk");
+  static_assert(kBwdImpEarly > 0 && kBwdImpEarly < kChunkBwd, "import lead within a chunk");
   const bool help_ok = KR == 1 && kDbl && !(a.flags & kFlagNoStorer) && B.nloc <= BS / 2 && B.nvirt <= BS / 2 &&
                        B.ncout * kChunkBwd <= BS / 2;
-  const bool imp_mode = help_ok && DDR_BWD_IMPWAVES && B.ncout > 0;
-  // x helpers (same blocks): the upper half also loads each reach's x(t - 4) row from x_save, DDR_BWD_XHELP_D
+  const bool imp_mode = help_ok && B.ncout > 0;
+  // x helpers (same blocks): the upper half also loads each reach's x(t - 4) row from x_save, kBwdHelpAhead
   // ticks ahead, and publishes it into the reach's slot, so the routing waves issue no x_save load and do
   // not wait at the tick's top for one
-#ifndef DDR_BWD_XHELP
-#define DDR_BWD_XHELP 1
-#endif
-#ifndef DDR_BWD_XHELP_D
-#define DDR_BWD_XHELP_D 3
-#endif
-  const bool xhelp = help_ok && DDR_BWD_XHELP;
+  const bool xhelp = help_ok;
   // gradient helpers (x-helper blocks, per-reach dL/drunoff, statics in registers): the same upper waves also
-  // load each reach's dL/drunoff[:, t] DDR_BWD_XHELP_D ticks ahead and publish it into a parity-indexed LDS row
+  // load each reach's dL/drunoff[:, t] kBwdHelpAhead ticks ahead and publish it into a parity-indexed LDS row
   // (the statics table's space, unused when the statics live in registers), so the routing waves issue no
   // global load and wait for none at the tick's top (a cold 16-B group load, one tick ahead, paced the light
   // backward: profiles/r05/ab_r05.txt item 12)
-#ifndef DDR_BWD_GHELP
-#define DDR_BWD_GHELP 1
-#endif
-  const bool ghelp = DDR_BWD_GHELP && kStatReg && kShiftG && xhelp && !(gauge);
+  const bool ghelp = kStatReg && kShiftG && xhelp && !(gauge);
   R* const sg = reinterpret_cast<R*>(sx + kXB * S);  // [2][S] (ghelp): dL/drunoff of each reach's step, by tick parity
   // virtual inflow owners (tid < nvirt): v_edge, v_off in registers; in LDS (own[tid], registers are
   // full) the virtual's consumer slot (low 16 bits) and the tick offset of cut-out `tid` (high 16 bits,
@@ -1356,7 +1218,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // compiler hoists above the vec4 branch, run by the whole wave every tick) are dropped -- at KR = 4 (at
     // KR = 1 the light C5-shaped backward measured 6 % slower without them, r05_nc0)
     auto cl = [&](int64_t i) {
-      return (!un && DDR_BWD_GRAD_NOCLAMP && KR >= 4) ? i : (i < 0 ? int64_t(0) : (i < T ? i : T - 1));
+      return (!un && KR >= 4) ? i : (i < 0 ? int64_t(0) : (i < T ? i : T - 1));
     };
     const int64_t i0 = cl(base), i1 = cl(base + 1), i2 = cl(base + 2), i3 = cl(base + 3);
     // m0: the gauge's t = 0 sum passed its clamp (state gradients only; mmc.py:398-412)
@@ -1409,17 +1271,6 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       return make_grad4(v0, v1, v2, v3);
     }
     // one reach row: the loaded values as they are
-#ifndef DDR_EXP_GRAD_DUMMY
-#define DDR_EXP_GRAD_DUMMY 0  // timing experiment only: dL/drunoff read from a 256-KB L2-resident window (wrong values)
-#endif
-    if (DDR_EXP_GRAD_DUMMY) {
-      const R* dm = gout + ((int64_t)(ref & 1023) << 6);
-      base &= 60;
-      if constexpr (sizeof(R) == 4) {
-        const float4 v = *reinterpret_cast<const float4*>(dm + base);
-        return make_grad4(v.x, v.y, v.z, v.w);
-      }
-    }
     return raw_row(gout + (int64_t)ref * T);
   };
   // ... plus the state seeds of steps T - 1 and T - 2 (a.gseed).  Only outside the steady ticks (seeded: the
@@ -1560,8 +1411,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       if (vown) vxn = load_virt((int64_t)tau - 1 - v_off - 2);  // the virtual's value for the next tick
     }
     // ---- compute ------------------------------------------------------------------------------
-    // per slice: the step's inputs (pre), its adjoint, its outputs (post) and the next loads (tail);
-    // NPB slices at a time share one packed adjoint (adjoint_step_fast2) when NPB = 2
+    // per slice: the step's inputs (pre), its adjoint, its outputs (post) and the next loads (tail)
     struct Pre {
       int r, rs, t;
       bool hk, active, c0;
@@ -1610,30 +1460,27 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         if (kStatReg && ghelp) P.gk = sg[(tb & 1) * S + P.rs];  // published by the gradient helpers last tick
       } else {
         const int e4 = P.t & 3;
-        if constexpr (DDR_BWD_SEL_BITS) {
-          // two bit tests, three selects (the ternary chain on e4 compiles into divergent branches)
-          const bool b0 = (e4 & 1) != 0, b1 = (e4 & 2) != 0;
-          const R lo = b0 ? g1[k] : g0[k], hi = b0 ? g3[k] : g2[k];
-          P.gk = b1 ? hi : lo;
-        } else {
-          P.gk = e4 == 0 ? g0[k] : (e4 == 1 ? g1[k] : (e4 == 2 ? g2[k] : g3[k]));  // dL/drunoff[:, t]
-        }
+        // dL/drunoff[:, t] by two bit tests and three selects (a ternary chain on e4 compiles into divergent
+        // branches)
+        const bool b0 = (e4 & 1) != 0, b1 = (e4 & 2) != 0;
+        const R lo = b0 ? g1[k] : g0[k], hi = b0 ? g3[k] : g2[k];
+        P.gk = b1 ? hi : lo;
       }
       P.xtk = xc[k];
-      P.st = kStatReg ? sreg[k] : tab.template get<!DDR_BWD_EXACT>(P.rs);
+      P.st = kStatReg ? sreg[k] : tab.template get<true>(P.rs);
       P.lm = lam[k] + P.gk;                                 // dL/dQ_t (+ dL/dout[:, t])
       const R gx = (P.xtk >= cs.qlb) ? P.lm : R(0);         // clamp backward (inclusive)
       P.gb64 = (double)gx + (double)A[k];                   // (I - C1 N)^T gb = gx (utils.py:188-242)
       P.gb = R(P.gb64);
       P.Qp = c0 ? xa[k] : rmaxc(xa[k], cs.qlb, cs);              // Q_{t-1}
       if constexpr (kDF) {
-        const SxT Qq = (SxT)P.Qp - (SxT)(DDR_EXP_DF_NOQ ? R(0) : rmaxc(qsv[kQs ? k : 0], cs.qlb, cs));  // exact in fp64
+        const SxT Qq = (SxT)P.Qp - (SxT)rmaxc(qsv[kQs ? k : 0], cs.qlb, cs);  // exact in fp64
         P.D1 = R(Qq - Sx);
         P.D2 = R(Qq - I);
       }
     };
     auto adjoint = [&](int k, const Pre& P, AdjOutR<R>& o) {
-      if constexpr (std::is_same<R, float>::value && !DDR_BWD_EXACT) {
+      if constexpr (std::is_same<R, float>::value) {
         AdjOut f;
         if constexpr (kDF) f = adjoint_step_fast<true>(P.st, P.Qp, cs, P.gb, P.D1, P.D2, R(0));
         else f = adjoint_step_fast<false>(P.st, P.Qp, cs, P.gb, P.xtk, P.Sx, P.I);
@@ -1642,10 +1489,10 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         const R qvk = *qs_at<R>(a, B, xs_base, tau, off_of(k), P.rs);  // q'[t-1] * flow_scale
         R tw, ss;
         Geom<R> geo;
-        coefficients<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, o.c1, o.c2, o.c3, o.c4, tw, ss, &geo);
+        coefficients<R, true>(P.st, P.Qp, cs, o.c1, o.c2, o.c3, o.c4, tw, ss, &geo);
         const R qc = rmaxc(qvk, cs.qlb, cs);
         const R gc1 = P.gb * P.Sx, gc2 = P.gb * P.I, gc3 = P.gb * P.Qp, gc4 = P.gb * qc;
-        coefficients_vjp<R, !DDR_BWD_EXACT>(P.st, P.Qp, cs, geo, o.c1, o.c2, o.c3, o.c4, gc1, gc2, gc3, gc4, o.gQ, o.gn,
+        coefficients_vjp<R, true>(P.st, P.Qp, cs, geo, o.c1, o.c2, o.c3, o.c4, gc1, gc2, gc3, gc4, o.gQ, o.gn,
                                             o.gq, o.gp);
       }
     };
@@ -1701,39 +1548,15 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
       }
     };
 #pragma unroll
-    for (int k0 = 0; k0 < KR; k0 += NPB) {
-      if (wbase + k0 * BS >= B.nloc) continue;
-      if constexpr (KR == 4) set_prio(KR - 1 - k0);
-      Pre P[NPB];
-#pragma unroll
-      for (int h = 0; h < NPB; ++h) pre(k0 + h, P[h]);
-      // the step's adjoint only where some lane of the wave runs a step this tick (DDR_SKIP_IDLE_BWD)
-      bool any = false;
-#pragma unroll
-      for (int h = 0; h < NPB; ++h) any = any || P[h].active || (GS && P[h].hk && P[h].t == 0);
-      const bool wave_act = !DDR_SKIP_IDLE_BWD || __builtin_amdgcn_ballot_w64(any) != 0;
-      if (wave_act) {
-        AdjOutR<R> o[NPB];
-        if constexpr (NPB == 2) {
-          // two slices' adjoint steps in packed halves (the same bits as two scalar steps)
-          AdjOut f0, f1;
-          if constexpr (kDF)
-            adjoint_step_fast2<true>(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].D1, P[0].D2, 0.0f},
-                                     AdjIn{P[1].Qp, P[1].gb, P[1].D1, P[1].D2, 0.0f}, cs, f0, f1);
-          else
-            adjoint_step_fast2<false>(P[0].st, P[1].st, AdjIn{P[0].Qp, P[0].gb, P[0].xtk, P[0].Sx, P[0].I},
-                                      AdjIn{P[1].Qp, P[1].gb, P[1].xtk, P[1].Sx, P[1].I}, cs, f0, f1);
-          o[0] = AdjOutR<R>{f0.c1, f0.c2, f0.c3, f0.c4, f0.gQ, f0.gn, f0.gq, f0.gp};
-          o[1] = AdjOutR<R>{f1.c1, f1.c2, f1.c3, f1.c4, f1.gQ, f1.gn, f1.gq, f1.gp};
-        } else {
-#pragma unroll
-          for (int h = 0; h < NPB; ++h) adjoint(k0 + h, P[h], o[h]);
-        }
-#pragma unroll
-        for (int h = 0; h < NPB; ++h) post(k0 + h, P[h], o[h]);
-      }
-#pragma unroll
-      for (int h = 0; h < NPB; ++h) tail(k0 + h, P[h]);
+    for (int k = 0; k < KR; ++k) {
+      if (wbase + k * BS >= B.nloc) continue;
+      if constexpr (KR == 4) set_prio(KR - 1 - k);
+      Pre P;
+      pre(k, P);
+      AdjOutR<R> o;
+      adjoint(k, P, o);
+      post(k, P, o);
+      tail(k, P);
       __builtin_amdgcn_sched_barrier(0);
     }
     phz.mark(4);  // loads issue + compute
@@ -1815,11 +1638,11 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     // import waves: thread w owns (cut-out w / kChunkBwd, step slot w % kChunkBwd) of every chunk; per tick
     // the same barriers as the routing waves' tick (the ring hand-off at a chunk boundary, the tick's end).
     // x helpers: thread w < nloc publishes reach w's x(t - 4) (forward row TT - 4 - tb at tick tb, clamped)
-    // into the next tick's x buffer, its loads issued DDR_BWD_XHELP_D ticks ahead
+    // into the next tick's x buffer, its loads issued kBwdHelpAhead ticks ahead
     const int w = tid - BS / 2;
     const bool wown = imp_mode && w < B.ncout * kChunkBwd;
     const bool xown = xhelp && w < B.nloc;
-    constexpr int XD = DDR_BWD_XHELP_D;
+    constexpr int XD = kBwdHelpAhead;
     const R* xcol = xsave + xs_base + (xown ? w : 0);
     auto xload = [&](int tb) -> R {
       int tc = TT - 4 - tb;
@@ -1874,8 +1697,8 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
         sg[((tb + 1) & 1) * S + w] = gr;
         gr = ghelp_load(grf, goff, tb + XD);
       }
-      const int nb = tb + DDR_BWD_IMP_EARLY;
-      if (DDR_BWD_IMP_EARLY > 0 && wown && (nb % kChunkBwd) == 0 && nb < TT) {
+      const int nb = tb + kBwdImpEarly;
+      if (wown && (nb % kChunkBwd) == 0 && nb < TT) {
         const int t = step_of(nb);
         if (t >= tmin && t < T) {
           const double* row = prow + (int64_t)t * 2;
@@ -1906,7 +1729,7 @@ __global__ void __launch_bounds__(kBlockThreads, kBlocksPerCU * kBlockThreads / 
     b0 += b0 & 1;
     b1 &= ~1;
   }
-  if (!DDR_BWD_STEADY || (a.flags & kFlagNoSteady) || b1 <= b0) b0 = b1 = 0;
+  if ((a.flags & kFlagNoSteady) || b1 <= b0) b0 = b1 = 0;
   if constexpr (kEarly) {
 #pragma unroll 1
     for (int tb = 0; tb < b0; tb += 2) {
@@ -1994,66 +1817,93 @@ __global__ void nan_last_row_kernel(RouteArgs a) {
   flag_nan(a, nan);
 }
 
-template <typename R, int G, int BS>
-__global__ void __launch_bounds__(BS) gather_qprime_kernel(RouteArgs a) {
+// One workgroup per (block, chunk of `chunk` steps, a multiple of G), G steps per LDS tile: each thread keeps
+// its reaches' reference indices, LDS destinations, tick offsets and scale in registers for the whole chunk
+// (a workgroup per tile re-read them: 12 B per reach per tile, a third of the q' bytes at G = 8), and the
+// next tile's q' loads are in flight while the current tile leaves LDS for the schedule rows.  A chunk's
+// tiles run on one CU back to back, so a tick row's segments written by consecutive tiles meet in its L2.
+template <typename R, int G, int BS, int KG>
+__global__ void __launch_bounds__(BS) gather_qprime_kernel(RouteArgs a, int chunk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
   R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
   if (a.owned && !a.owned[blockIdx.x]) return;  // split basin: another rank's block
   const BlockDesc B = a.s.blocks[blockIdx.x];
   const int64_t T = a.T, N = a.N;
-  const int64_t t0 = (int64_t)blockIdx.y * G;
+  const int64_t tA = (int64_t)blockIdx.y * chunk;
+  if (tA >= T) return;
+  const int64_t tB = tA + chunk < T ? tA + chunk : T;
   const int nl = B.nloc;
+  const int tid = threadIdx.x;
   const R* qp = static_cast<const R*>(a.qprime);
   const R* fs = static_cast<const R*>(a.fs);
-  const int* rs_loc = a.s.rs_loc + B.pos0;
-  const int* rs_ref = a.s.rs_ref + B.pos0;
-  // q' row of step t = t0 + j (t clamped into [0, T)): max(t - shift, 0) -- step t routes q'[t - 1]
-  // (mmc.py:421-424), shift 0 in accumulation mode -- divided by the hours per stored row (24 for a
-  // daily store: the reader's repeat(24), readers.py:513-519)
-  int64_t rowoff[G];
+  const unsigned char* valid = a.qp_valid;
+  // read side (ascending reference order: runs of adjacent q' columns) and write side (positions, sorted by
+  // tick offset: runs of one offset are contiguous in a tick row)
+  int ref[KG], loc[KG];
+  int64_t off[KG];
+  R sc[KG];
+  bool fill[KG];
 #pragma unroll
-  for (int j = 0; j < G; ++j) {
-    int64_t t = t0 + j;
+  for (int k = 0; k < KG; ++k) {
+    const int i = tid + k * BS;
+    const bool h = i < nl;
+    ref[k] = h ? a.s.rs_ref[B.pos0 + i] : 0;
+    loc[k] = h ? a.s.rs_loc[B.pos0 + i] : 0;
+    off[k] = h ? a.s.off[B.pos0 + i] : 0;
+    sc[k] = fs ? fs[ref[k]] : R(1);
+    fill[k] = valid && !valid[ref[k]];  // a divide missing from the store: the reader's 0.001 fill (readers.py:523-530)
+  }
+  // q' row of step t (t clamped into [0, T)): max(t - shift, 0) -- step t routes q'[t - 1] (mmc.py:421-424),
+  // shift 0 in accumulation mode -- divided by the hours per stored row (readers.py:513-519)
+  auto rowoff = [&](int64_t t) {
     t = t < T ? t : T - 1;
     t = t > a.qp_shift ? t - a.qp_shift : 0;
-    rowoff[j] = (t / a.qp_hours) * N;
-  }
-  const unsigned char* valid = a.qp_valid;
-  bool nan = false;
-  // all G loads of a reach are independent and issued together (memory-level parallelism)
-#pragma unroll 2
-  for (int i = threadIdx.x; i < nl; i += BS) {
-    const int ref = rs_ref[i], loc = rs_loc[i];
-    R v[G];
-#pragma unroll
-    for (int j = 0; j < G; ++j) v[j] = qp[rowoff[j] + ref];
-    if (valid && !valid[ref]) {
-      // a divide missing from the store: the reader's 0.001 fill (readers.py:523-530)
-#pragma unroll
-      for (int j = 0; j < G; ++j) v[j] = R(0.001f);
-    }
-    if (fs) {
-      const R f = fs[ref];
-#pragma unroll
-      for (int j = 0; j < G; ++j) v[j] = v[j] * f;
-    }
+    return (t / a.qp_hours) * N;
+  };
+  R v[KG][G];
+  auto load = [&](int64_t t0) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      tile[j * nl + loc] = v[j];
-      nan = nan || v[j] != v[j];
+      const R* row = qp + rowoff(t0 + j);
+#pragma unroll
+      for (int k = 0; k < KG; ++k)
+        if (tid + k * BS < nl) v[k][j] = row[ref[k]];
     }
+  };
+  R* qs = static_cast<R*>(a.qs) + T * B.pos0 + B.pre_dn;
+  bool nan = false;
+  load(tA);
+#pragma unroll 1
+  for (int64_t t0 = tA; t0 < tB; t0 += G) {
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      if (tid + k * BS >= nl) continue;
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        R x = fill[k] ? R(0.001f) : v[k][j];
+        if (fs) x = x * sc[k];
+        tile[j * nl + loc[k]] = x;
+        nan = nan || x != x;
+      }
+    }
+    __syncthreads();
+    if (t0 + G < tB) load(t0 + G);  // lands while this tile is written out
+    const int jn = (int)(tB - t0 < G ? tB - t0 : G);
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int r = tid + k * BS;
+      if (r >= nl) continue;
+      R* col = qs + (t0 + off[k]) * nl + r;
+      if (jn == G) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) col[(int64_t)j * nl] = tile[j * nl + r];
+      } else {
+        for (int j = 0; j < jn; ++j) col[(int64_t)j * nl] = tile[j * nl + r];
+      }
+    }
+    __syncthreads();
   }
   flag_nan(a, nan);
-  __syncthreads();
-  R* qs = static_cast<R*>(a.qs) + T * B.pos0 + B.pre_dn;
-  const int* off = a.s.off + B.pos0;
-  const int jn = (int)(T - t0 < G ? T - t0 : G);
-  for (int r = threadIdx.x; r < nl; r += BS) {
-    const int64_t o = off[r];
-#pragma unroll
-    for (int j = 0; j < G; ++j)
-      if (j < jn) qs[(t0 + j + o) * nl + r] = tile[j * nl + r];
-  }
 }
 
 // Adjoint of gather_qprime: dL/dq'[s, ref] = flow_scale[ref] * sum over the steps t reading row s
@@ -2268,11 +2118,7 @@ const void* backward_kernel_of(const Graph* g, bool gs, bool df = false, int pl 
 }
 // the plain backward instance a launch can take (route_backward_kernel's PL), 0 when none
 inline int backward_plain_of(const Graph* g, const RouteArgs& a) {
-  static const bool ok = [] {
-    const char* v = getenv("DDR_BWD_PLAIN");
-    return v == nullptr || atoi(v) != 0;
-  }();
-  if (!ok || g->split.nranks > 0 || a.prof != nullptr || a.gseed != nullptr || (a.T & 3) != 0) return 0;
+  if ((a.flags & kFlagNoPlain) || g->split.nranks > 0 || a.prof != nullptr || a.gseed != nullptr || (a.T & 3) != 0) return 0;
   // gauge mode only: c3s8 backward -4.5 %; per-reach dL/drunoff (PL = 1) measured 0.5-1.5 % slower at C5 and
   // 3 % at light load (r05_plain3, r05_pl1), so that instance is not built
   return a.g_roff != nullptr ? 2 : 0;
@@ -2318,10 +2164,7 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
     size_t fsmem = smem;
     if constexpr (std::is_same<R, float>::value) {
       // the plain instance (route_forward_kernel's PL) this launch can take: 0 none, 1 runoff rows, 2 none written
-      static const bool plain_ok = [] {
-        const char* v = getenv("DDR_FWD_PLAIN");
-        return v == nullptr || atoi(v) != 0;
-      }();
+      const bool plain_ok = !(a.flags & kFlagNoPlain);
       const bool rows = a.runoff != nullptr && !(a.flags & DDR_FWD_NO_RUNOFF);
       int plain = 0;
       if (plain_ok && g->split.nranks == 0 && a.prof == nullptr && !(a.flags & DDR_FWD_ACCUMULATE)) {
@@ -2333,14 +2176,10 @@ hipError_t launch_route_kr(const Graph* g, RouteArgs a, bool backward, hipStream
       // KR = 4 (faithful): double-buffered x slots -- one barrier per tick -- where this graph's largest
       // block leaves the LDS for a second buffer (C5's blocks of <= ~3800 reaches; C3's 4096 do not)
       if constexpr (KR == 4) {
-        static const bool dbl4 = [] {
-          const char* v = getenv("DDR_FWD_DBL4");
-          return v == nullptr || atoi(v) != 0;
-        }();
         const size_t b2 = route_lds_bytes((size_t)route_slot_stride(g->max_slots), (size_t)g->max_virt,
                                           (size_t)g->max_cout, (size_t)g->max_xl, false, sizeof(R), g->kr, 2);
         const size_t s2 = align16(b2) + split_table_bytes(g, false);
-        if (dbl4 && (a.flags & DDR_FWD_FAITHFUL_MATH) && s2 <= kLdsBudget) {
+        if ((a.flags & DDR_FWD_FAITHFUL_MATH) && s2 <= kLdsBudget) {
           kern = forward_faithful_of<R, KR, 2>(plain);
           fsmem = s2;
           a.xl_off = (int32_t)(b2 - (size_t)g->max_xl * 4);
@@ -2459,10 +2298,7 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-#ifndef DDR_GATHER_G
-#define DDR_GATHER_G 8
-#endif
-  constexpr int G = sizeof(R) == 4 ? DDR_GATHER_G : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
+  constexpr int G = sizeof(R) == 4 ? 8 : 4;  // G * 4096 reaches * sizeof(R) <= 128 KiB of LDS
   const size_t smem = (size_t)G * g->max_nloc * sizeof(R);
   if (a.qs_rows > 0) {
     auto rk = gather_qprime_rows_kernel<R, G>;
@@ -2472,27 +2308,31 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
                        stream, a);
     return hipGetLastError();
   }
-  // light loads (small blocks): more steps per workgroup and 256-thread workgroups -- a workgroup of
-  // 8 steps over a few hundred reaches moved ~20 KB, and the launch was paced by workgroup turnover
-  // (3.2 ms for a 69k-reach C5 shard, 1.5 TB/s)
+  // workgroups of (block, chunk of kTilesPerChunk tiles): short enough that the dispatcher balances blocks of
+  // unequal size (a chunk of ~1000 steps left a ~1.5-ms tail behind the largest blocks), long enough that the
+  // per-chunk index reads are a small fraction of the q' bytes
   auto launch = [&](auto kern, int gsteps, int bs) -> hipError_t {
     const size_t sm = (size_t)gsteps * g->max_nloc * sizeof(R);
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     if (e != hipSuccess) return e;
-    const dim3 grid((unsigned)g->blocks.size(), (unsigned)((a.T + gsteps - 1) / gsteps));
-    hipLaunchKernelGGL(kern, grid, dim3(bs), sm, stream, a);
+    constexpr int64_t kTilesPerChunk = 4;  // C5: 13.35 ms (2: 13.34, 8: 13.45, 16: 13.73; r05's tile per workgroup 13.92)
+    const int64_t nb = (int64_t)g->blocks.size();
+    const int64_t chunk = kTilesPerChunk * gsteps;
+    const int64_t y = (a.T + chunk - 1) / chunk;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nb, (unsigned)y), dim3(bs), sm, stream, a, (int)chunk);
     return hipGetLastError();
   };
-  static const int gsel = [] {
-    const char* v = getenv("DDR_GATHER_SEL");
-    return v ? atoi(v) : 1;
-  }();
   if constexpr (sizeof(R) == 4) {
-    if (gsel && g->max_nloc <= 256) return launch(gather_qprime_kernel<R, 32, 256>, 32, 256);
-    if (gsel && g->max_nloc <= 512) return launch(gather_qprime_kernel<R, 32, 512>, 32, 512);
-    if (gsel && g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, 16, 1024>, 16, 1024);
+    if (g->max_nloc <= 256) return launch(gather_qprime_kernel<R, 32, 256, 1>, 32, 256);
+    if (g->max_nloc <= 512) return launch(gather_qprime_kernel<R, 32, 512, 1>, 32, 512);
+    if (g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, 16, 1024, 1>, 16, 1024);
+    if (g->max_nloc <= 2048) return launch(gather_qprime_kernel<R, 16, 1024, 2>, 16, 1024);
+    return launch(gather_qprime_kernel<R, G, 1024, 4>, G, 1024);
+  } else {
+    if (g->max_nloc <= 1024) return launch(gather_qprime_kernel<R, G, 1024, 1>, G, 1024);
+    if (g->max_nloc <= 2048) return launch(gather_qprime_kernel<R, G, 1024, 2>, G, 1024);
+    return launch(gather_qprime_kernel<R, G / 2, 1024, 4>, G / 2, 1024);  // (G = 4: spills at four reaches)
   }
-  return launch(gather_qprime_kernel<R, G, 1024>, G, 1024);
 }
 
 template <typename R>

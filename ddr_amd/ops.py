@@ -313,18 +313,16 @@ def _geometry_vjp(ctx, n, q, p, slope, x_save, g_tw, g_ss):
     from .geometry.trapezoidal import compute_trapezoidal_geometry
 
     T = ctx.steps
-    carry = bool(ctx.flags & _lib.DDR_FWD_CARRY)
     if T < 2 or ctx.flags & _lib.DDR_FWD_ACCUMULATE:
         raise NotImplementedError("this launch reports no geometry (T < 2 or an accumulation launch)")
-    if T == 2 and carry:
-        # Q_0 is then the carried state itself, which the adjoint seeds through runoff[:, 0]'s clamp
-        raise NotImplementedError("geometry gradients of a 2-step carried window (use route_timestep's state)")
+    # (a carried 2-step window, route_timestep's: Q_{T-2} is the carried state itself, unclamped)
     qprev = state_at(ctx.graph, x_save, T, T - 2, ctx.consts[1], ctx.flags)
     with torch.enable_grad():
         Qv = qprev.detach().requires_grad_(True)
         nv, qv, pv = (t.detach().requires_grad_(True) for t in (n, q, p))
         geo = compute_trapezoidal_geometry(nv, pv, qv, Qv, slope, depth_lb=ctx.consts[4],
-                                           bottom_width_lb=ctx.consts[5])
+                                           bottom_width_lb=ctx.consts[5], side_slope_lb=ctx.consts[6],
+                                           side_slope_ub=ctx.consts[7])
         outs, gouts = [], []
         for key, gv in (("top_width", g_tw), ("side_slope", g_ss)):
             if gv is not None:
@@ -344,16 +342,23 @@ def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
     geo = nz(g_tw) or nz(g_ss)
     # per-reach state seeds (ddr_mc_backward_ex): row 0 dL/dQ_{T-1} = dL/d_discharge_t (an autograd tensor in
     # the reference in gauge mode too, mmc.py:433-441), row 1 dL/dQ_{T-2} from the reported geometry's VJP
+    # A carried 2-step window (route_timestep, mmc.py:487-559): Q_{T-2} = Q_0 is the carried state, which the
+    # geometry reads unclamped -- its VJP goes straight into dL/dQ0, not through the adjoint's step-0 seed
+    # (which is runoff[:, 0]'s clamp)
+    geo_q0 = geo and T == 2 and bool(ctx.flags & _lib.DDR_FWD_CARRY)
     gseed = None
-    if g_qlast is not None or geo:
+    if g_qlast is not None or (geo and not geo_q0):
         gseed = torch.zeros((2, N), device=qprime.device, dtype=qprime.dtype)
         if g_qlast is not None:
             gseed[0] = g_qlast
-    extra = None
+    extra, gQ_geo = None, None
     if geo:
         gQ, gn2, gq2, gp2 = _geometry_vjp(ctx, n, q, p, slope, x_save, g_tw if nz(g_tw) else None,
                                           g_ss if nz(g_ss) else None)
-        gseed[1] = gQ
+        if geo_q0:
+            gQ_geo = gQ
+        else:
+            gseed[1] = gQ
         extra = (gn2, gq2, gp2)
     if g_runoff is None:
         G = g_off.numel() - 1 if ctx.gauge else N
@@ -371,6 +376,8 @@ def _backward(ctx, g_runoff, g_qlast, g_tw, g_ss, g_xsave, g_bnd):
         gn = gn + extra[0]
         gq = gq + extra[1]
         gp = gp + extra[2].reshape(gp.shape)
+    if want_q0 and gQ_geo is not None:
+        gq0 = gq0 + gQ_geo
     return ((gqp if want_qp else None), gn, gq, gp) + (None,) * 4 + ((gq0 if want_q0 else None),) + (None,) * 11
 
 

@@ -65,6 +65,17 @@ def denorm_table(ranges: dict, log_space=("p_spatial",)) -> list[float]:
     return rows
 
 
+def _check_device_f32(t: torch.Tensor, dev: torch.device, what: str, shape=None) -> None:
+    """The C ABI takes raw device pointers: a host, fp64, strided or other-device tensor would be read as
+    fp32 device memory (a GPU memory fault, not a Python error), so reject it here."""
+    if not (t.is_cuda and t.device == dev):
+        raise ValueError(f"the fused parameter network's {what} must be on {dev} (got {t.device})")
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise ValueError(f"the fused parameter network's {what} must be contiguous float32")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"the fused parameter network's {what} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+
+
 class _PnetFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, flat, table):
@@ -88,7 +99,9 @@ class _PnetFn(torch.autograd.Function):
         lib = _lib.load()
         N, F = x.shape
         dev = x.device
-        g = [t.contiguous() if t is not None else torch.zeros(N, device=dev) for t in (gn, gq, gp)]
+        g = [t.to(torch.float32).contiguous() if t is not None else torch.zeros(N, device=dev) for t in (gn, gq, gp)]
+        for t in g:
+            _check_device_f32(t, dev, "output gradient", (N,))
         grad = torch.empty_like(flat)
         work = torch.empty(max(int(lib.ddr_pnet_work_bytes(N, F)), 4), device=dev, dtype=torch.uint8)
         tab = (C.c_float * 9)(*ctx.table)
@@ -115,6 +128,9 @@ class ParamNet(torch.nn.Module):
         x = x.to(torch.float32).contiguous()
         if x.dim() != 2 or x.shape[1] != self.n_features:
             raise ValueError(f"attributes must be (N, {self.n_features})")
+        # the parameters as the kernels read them: fp32, contiguous, on x's device (not after .double() or
+        # without .to(device))
+        _check_device_f32(self.flat, x.device, "parameters", (param_count(self.n_features),))
         return _PnetFn.apply(x, self.flat, self.table)
 
 

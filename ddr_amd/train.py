@@ -60,7 +60,11 @@ def daily_l1_loss(daily: torch.Tensor, obs: torch.Tensor, warmup: int, inv_count
 class ClipAdam:
     """``clip_grad_norm_(max_norm)`` then ``torch.optim.Adam(lr, betas, eps)`` (no weight decay) on one flat
     fp32 parameter tensor, in two launches per step (64 workgroups).  ``max_norm`` <= 0 disables clipping.  ``last_norm`` holds the
-    gradient norm of the last step (a device scalar, clip_grad_norm_'s return value)."""
+    gradient norm of the last step (a device scalar, clip_grad_norm_'s return value).
+
+    Unlike ``torch.nn.utils.clip_grad_norm_``, the clip is applied inside the update only: ``param.grad`` keeps
+    the unclipped gradient after :meth:`step` (code that reads or accumulates ``.grad`` afterwards sees the raw
+    gradient, not the reference loop's clipped one, ``scripts/train.py:99-100``)."""
 
     def __init__(self, param: torch.Tensor, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  max_norm: float = 1.0):

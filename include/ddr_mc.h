@@ -462,8 +462,11 @@ ddr_status ddr_graph_clear_split(ddr_graph* g);
  * times out (tests the failure path).  DDR_DEBUG_NO_STEADY: the routing kernels run every tick
  * through their general path instead of the specialised steady-tick path (bitwise A/B; also set by
  * the environment variable DDR_NO_STEADY=1).  DDR_DEBUG_NO_STORER: light forward blocks store the
- * routing state and runoff from their compute waves instead of their idle waves (DDR_NO_STORER=1). */
-enum { DDR_DEBUG_FORCE_TIMEOUT = 1, DDR_DEBUG_NO_STEADY = 2, DDR_DEBUG_NO_STORER = 4 };
+ * routing state and runoff from their compute waves instead of their idle waves (DDR_NO_STORER=1).
+ * DDR_DEBUG_NO_PLAIN: launches without the rare options (split basin, profile, state seeds, daily
+ * accumulation) run the general kernel instances instead of the plain ones compiled without those options
+ * (bitwise A/B; DDR_NO_PLAIN=1). */
+enum { DDR_DEBUG_FORCE_TIMEOUT = 1, DDR_DEBUG_NO_STEADY = 2, DDR_DEBUG_NO_STORER = 4, DDR_DEBUG_NO_PLAIN = 8 };
 ddr_status ddr_set_debug_flags(int32_t flags);
 
 /* General sparse triangular solve A x = b (lower) or A^T x = b (transpose = 1), CSR A with a

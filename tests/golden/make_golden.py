@@ -28,6 +28,8 @@ Fixtures:
   chain.npz     F12 gradients out of the final state and the reported geometry: two chained gauge-mode
                     batches (the second carries the first's _discharge_t with its graph), and one batch
                     with the loss also on _discharge_t, top_width and side_slope (gauge / all-output mode)
+  timestep_geo.npz F13 a 3-step route_timestep chain whose loss includes every step's top_width /
+                    side_slope (the geometry of the carried state, two carried values below q_lb)
   daily.npz     F8  the training objective of scripts/train.py:78-97 on a (7, 2136) gauge series:
                     downsample(runoff[:, 13:-8], 88) (io/functions.py:7-23), NaN-gauge mask, L1 with
                     warmup 3, and torch autograd's d loss / d runoff
@@ -515,11 +517,53 @@ def make_chain():
     np.savez_compressed(HERE / "chain.npz", **out)
 
 
+def make_timestep_geo():
+    """F13: a 3-step ``route_timestep`` chain (the BMI update) whose loss includes every step's reported
+    ``top_width`` / ``side_slope`` -- the geometry of the carried ``_discharge_t`` the step starts from
+    (mmc.py:527-538, 161-162), so the geometry's gradient reaches the carried state, unclamped (two carried
+    values below q_lb), and through it every earlier step."""
+    _, mmc = load_reference()
+    net = synthetic.random_binary_tree(90, seed=41)
+    attrs = synthetic.reach_attributes(net.n, 41)
+    u = synthetic.unit_parameters(net.n, 41)
+    rng = np.random.default_rng(4100)
+    dc = routing_dc(net.n, net.rows, net.cols, attrs)
+    mc = mmc.MuskingumCunge(cfg_of(PARAMS_DEFAULT), device="cpu")
+    sp = {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in u.items()}
+    qc = synthetic.lateral_inflow(net.n, 3, 41)
+    mc.setup_inputs(dc, torch.from_numpy(qc), sp)
+    q0 = rng.uniform(0.5, 5.0, net.n).astype(np.float32)
+    q0[[7, 30]] = np.float32(2e-5)
+    s0 = torch.from_numpy(q0).clone().requires_grad_(True)
+    mc._discharge_t = s0
+    mapper, _, _ = mc.create_pattern_mapper()
+    W = rng.uniform(0, 1, (3, net.n)).astype(np.float32)
+    V = rng.uniform(-1, 1, (3, 2, net.n)).astype(np.float32)
+    qcl = [torch.from_numpy(np.maximum(qc[k], np.float32(1e-4))).clone().requires_grad_(True) for k in range(3)]
+    loss = 0.0
+    states, tws, sss = [], [], []
+    for k in range(3):
+        q1 = mc.route_timestep(q_prime_clamp=qcl[k], mapper=mapper)
+        loss = loss + (q1 * torch.from_numpy(W[k])).sum() + (mc.top_width * torch.from_numpy(V[k, 0])).sum() \
+            + (mc.side_slope * torch.from_numpy(V[k, 1])).sum()
+        states.append(q1.detach().numpy().copy())
+        tws.append(mc.top_width.detach().numpy().copy())
+        sss.append(mc.side_slope.detach().numpy().copy())
+        mc._discharge_t = q1
+    loss.backward()
+    np.savez_compressed(HERE / "timestep_geo.npz", n=np.int64(net.n), rows=net.rows, cols=net.cols,
+                        length=attrs.length, slope=attrs.slope, x=attrs.x, **{f"u_{k}": v for k, v in u.items()},
+                        qprime=qc, q0=q0, W=W, V=V, ref_states=np.stack(states), ref_top_width=np.stack(tws),
+                        ref_side_slope=np.stack(sss), ref_grad_q0=s0.grad.numpy().copy(),
+                        ref_grad_qclamp=np.stack([q.grad.numpy().copy() for q in qcl]),
+                        **{f"ref_grad_{k}": v.grad.numpy().copy() for k, v in sp.items()})
+
+
 def main():
     if len(sys.argv) > 1:
         for name in sys.argv[1:]:
             {"geostats": make_geostats, "daily": make_daily, "collate": make_collate, "deep": make_deep,
-             "state": make_state, "chain": make_chain}[name]()
+             "state": make_state, "chain": make_chain, "timestep_geo": make_timestep_geo}[name]()
         return
     torch.manual_seed(0)
     utils, mmc = load_reference()
@@ -573,6 +617,7 @@ def main():
     make_daily()
     make_state()
     make_chain()
+    make_timestep_geo()
     for f in sorted(HERE.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

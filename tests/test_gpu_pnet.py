@@ -50,3 +50,19 @@ def test_fused_network_backward_is_deterministic(cuda):
         grads.append(net.flat.grad.clone())
     assert torch.equal(grads[0], grads[1])
     assert np.isfinite(grads[0].cpu().numpy()).all()
+
+
+def test_fused_network_rejects_misplaced_parameters(cuda):
+    """The C ABI takes raw pointers: parameters left on the host, cast to fp64 or on another device must raise
+    (a ValueError), not reach the kernel as fp32 device memory."""
+    ranges = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
+    x = torch.rand((1000, 10), device=cuda)
+    net = ParamNet(10, ranges)
+    with pytest.raises(ValueError):
+        net(x)  # parameters still on the host
+    net = net.to(cuda).double()
+    with pytest.raises(ValueError):
+        net(x)  # fp64 parameters
+    net = net.float()
+    outs = net(x)
+    assert all(o.shape == (1000,) for o in outs)

@@ -119,6 +119,53 @@ def test_route_timestep_chain_gradients_match_reference(cuda):
         assert normrel(sp_params[k].grad.cpu().numpy(), d[f"ref_c_grad_{k}"]) <= 5e-5, k
 
 
+def test_route_timestep_chain_geometry_gradients_match_reference(cuda):
+    """F13 (tests/golden/timestep_geo.npz): three chained route_timestep calls whose loss also takes every
+    step's reported top_width / side_slope -- the geometry of the carried state the step starts from
+    (mmc.py:527-538, 161-162; two carried values below q_lb, which the geometry reads unclamped).  Its gradient
+    reaches the carried state, each step's lateral inflow and the parameters as in the reference's autograd."""
+    from types import SimpleNamespace
+
+    import scipy.sparse as sp
+
+    from ddr_amd.routing.mmc import MuskingumCunge
+
+    d = load_golden("timestep_geo")
+    n = int(d["n"])
+    a = sp.coo_matrix((np.ones(len(d["rows"]), np.float32), (d["rows"], d["cols"])), shape=(n, n)).tocsr()
+    adj = torch.sparse_csr_tensor(torch.from_numpy(a.indptr.astype(np.int64)), torch.from_numpy(a.indices.astype(np.int64)),
+                                  torch.from_numpy(a.data), size=(n, n))
+    dc = SimpleNamespace(adjacency_matrix=adj, length=torch.from_numpy(d["length"]), slope=torch.from_numpy(d["slope"]),
+                         x=torch.from_numpy(d["x"]), top_width=torch.empty(0), side_slope=torch.empty(0),
+                         outflow_idx=None, gage_catchment=None, observations=None, flow_scale=None)
+    mc = MuskingumCunge(SimpleNamespace(params=SimpleNamespace(**PARAMS_DEFAULT)), device=cuda)
+    sp_params = {k: torch.from_numpy(d[f"u_{k}"]).to(cuda).requires_grad_(True) for k in ("n", "q_spatial", "p_spatial")}
+    mc.setup_inputs(dc, torch.from_numpy(d["qprime"]).to(cuda), sp_params)
+    s0 = torch.from_numpy(d["q0"]).to(cuda).requires_grad_(True)
+    mc._discharge_t = s0
+    mapper, _, _ = mc.create_pattern_mapper()
+    qcl = [torch.clamp(torch.from_numpy(d["qprime"][k]).to(cuda), min=1e-4).requires_grad_(True) for k in range(3)]
+    t = lambda a_: torch.from_numpy(a_).to(cuda)  # noqa: E731
+    loss = 0.0
+    states, tws, sss = [], [], []
+    for k in range(3):
+        q1 = mc.route_timestep(q_prime_clamp=qcl[k], mapper=mapper)
+        loss = loss + (q1 * t(d["W"][k])).sum() + (mc.top_width * t(d["V"][k, 0])).sum() \
+            + (mc.side_slope * t(d["V"][k, 1])).sum()
+        states.append(q1.detach().cpu().numpy())
+        tws.append(mc.top_width.detach().cpu().numpy())
+        sss.append(mc.side_slope.detach().cpu().numpy())
+        mc._discharge_t = q1
+    loss.backward()
+    assert maxrel(np.stack(states), d["ref_states"]) <= 1e-4
+    assert maxrel(np.stack(tws), d["ref_top_width"]) <= 1e-4
+    assert maxrel(np.stack(sss), d["ref_side_slope"]) <= 1e-4
+    assert normrel(s0.grad.cpu().numpy(), d["ref_grad_q0"]) <= 5e-5
+    assert normrel(np.stack([v.grad.cpu().numpy() for v in qcl]), d["ref_grad_qclamp"]) <= 5e-5
+    for k in ("n", "q_spatial", "p_spatial"):
+        assert normrel(sp_params[k].grad.cpu().numpy(), d[f"ref_grad_{k}"]) <= 5e-5, k
+
+
 @pytest.mark.parametrize("gkw", PARTITIONS, ids=["whole", "cut"])
 @pytest.mark.parametrize("mode", ["hot", "carry", "gauge_carry", "daily"])
 def test_fp64_state_gradients_match_fp64_oracle(cuda, gkw, mode):

@@ -85,3 +85,24 @@ def test_storer_waves_are_bitwise_the_compute_wave_stores(cuda, T):
         b = _run(case, cuda, g, "faithful", flags=_lib.DDR_DEBUG_NO_STORER, **kw)
         for k in a:
             assert np.array_equal(a[k], b[k], equal_nan=True), k
+
+
+@pytest.mark.parametrize("cap", [256, 1536, 4096], ids=["kr1", "kr2", "kr4"])
+def test_plain_instances_are_bitwise_the_general_ones(cuda, cap):
+    """Launches without the rare options (split basin, block profile, state seeds, daily accumulation) run
+    kernel instances compiled without them (route.hip, PL); outputs and gradients equal the general
+    instances' (DDR_DEBUG_NO_PLAIN) bit for bit, per-reach runoff and gauge mode, at one, two and four reaches
+    per thread."""
+    net = synthetic.forest(synthetic.loguniform_sizes(10, 200, 12000, 13), seed=13)
+    T = 200
+    case = synthetic_case(net, T, 13)
+    g = RiverGraph(net.n, net.rows, net.cols, max_block_reaches=cap, target_blocks=16)
+    assert g.info.reaches_per_thread == {256: 1, 1536: 2, 4096: 4}[cap]
+    outlets = np.flatnonzero(net.down < 0)
+    gz = GaugeMap.build([np.array([o]) for o in outlets], net.n, cuda)
+    for kw in ({}, {"gauges": gz}):
+        a = _run(case, cuda, g, "faithful", flags=0, **kw)
+        b = _run(case, cuda, g, "faithful", flags=_lib.DDR_DEBUG_NO_PLAIN, **kw)
+        for k in a:
+            assert np.array_equal(a[k], b[k], equal_nan=True), k
+

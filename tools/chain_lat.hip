@@ -6,7 +6,6 @@
 //   mode 2 fwd-faithful   coefficients_faithful (the default forward)
 //   mode 3 bwd            adjoint_step_fast with Q independent of the chain (the saved state), gb on it
 //   mode 4 sync only      a multiply-add, no physics
-//   mode 5 fwd-faithful2  two reaches per lane, coefficients_faithful2 (packed halves): ns per PAIR of steps
 // With lds = 1 each step also publishes its value to an LDS slot, passes a workgroup barrier and reads
 // a neighbour's slot (the tick's hand-off); lds = 0 keeps the chain in registers.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt \
@@ -44,13 +43,6 @@ __global__ void __launch_bounds__(1024) chain(int K, float* out, unsigned long l
       x = (double)(0.5f + o.gQ * 0.25f + o.gn * 1e-3f + o.gq * 1e-3f + o.gp * 1e-3f) + (double)o.c1 * xu;
     } else if constexpr (MODE == 4) {
       x = 0.999 * xu + (double)Q;
-    } else if constexpr (MODE == 5) {
-      PhysOut<float> p0, p1;
-      const float Q1 = Q * 0.75f + 0.01f * In;  // a second chain riding on the first
-      coefficients_faithful2(st, st, Q, Q1, cs, p0, p1);
-      const float b0 = ((p0.c2 * In) + (p0.c3 * Q)) + (p0.c4 * qc);
-      const float b1 = ((p1.c2 * In) + (p1.c3 * Q1)) + (p1.c4 * qc);
-      x = ((double)b0 + (double)p0.c1 * xu) + ((double)b1 + (double)p1.c1 * xu) * 1e-3;
     } else {
       PhysOut<float> ph;
       if constexpr (MODE == 1) {
@@ -111,13 +103,11 @@ int main(int argc, char** argv) {
     run<2, false>("fwd-faithful", K, W, out, clk);
     run<3, false>("bwd", K, W, out, clk);
     run<4, false>("sync-only", K, W, out, clk);
-    run<5, false>("fwd-faithful2", K, W, out, clk);
     run<0, true>("fwd-exact", K, W, out, clk);
     run<1, true>("fwd-fast", K, W, out, clk);
     run<2, true>("fwd-faithful", K, W, out, clk);
     run<3, true>("bwd", K, W, out, clk);
     run<4, true>("sync-only", K, W, out, clk);
-    run<5, true>("fwd-faithful2", K, W, out, clk);
   }
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }

@@ -21,7 +21,7 @@ for line in out.splitlines():
         k, v = s.split(":", 1)
         cur[k.strip()] = v.strip()
 for r in rows:
-    if "route_" not in r["name"]:
+    if "route_" not in r["name"] and "gather" not in r["name"]:
         continue
     n = r["name"].replace("_ZN3ddr", "").replace("EEEvNS_9RouteArgsE", "")
     print(f'{n:42s} VGPR {r.get("VGPRs","?"):>4} spillV {r.get("VGPRs Spill","?"):>4} '
