@@ -1873,10 +1873,12 @@ __global__ void __launch_bounds__(BS) gather_qprime_kernel(RouteArgs a, int chun
   }
   // q' row of step t (t clamped into [0, T)): max(t - shift, 0) -- step t routes q'[t - 1] (mmc.py:421-424),
   // shift 0 in accumulation mode -- divided by the hours per stored row (readers.py:513-519)
-  auto rowoff = [&](int64_t t) {
-    t = t < T ? t : T - 1;
-    t = t > a.qp_shift ? t - a.qp_shift : 0;
-    return (t / a.qp_hours) * N;
+  // (32-bit: T < 2^31; an int64 division is ~130 instructions per row, a branch around the row's loads)
+  const unsigned H = (unsigned)a.qp_hours, shift = (unsigned)a.qp_shift;
+  auto rowoff = [&](int64_t t64) {
+    unsigned t = (unsigned)(t64 < T ? t64 : T - 1);
+    t = t > shift ? t - shift : 0u;
+    return (int64_t)(H == 1u ? t : t / H) * N;
   };
   R v[KG][G];
   auto load = [&](int64_t t0) {
