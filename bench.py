@@ -253,6 +253,17 @@ def cpu_baseline(args, net_global, x_const):
     return out
 
 
+def split_factor() -> float:
+    """The largest basin is split over a rank group when it exceeds this multiple of a rank's share
+    (ddr_amd.split.plan_ranks; DDR_SPLIT_FACTOR overrides)."""
+    return float(os.environ.get("DDR_SPLIT_FACTOR", "1.2"))
+
+
+def shard_steps(T: int) -> int:
+    """T for the depth-aware basin assignment (distributed.shard_network); DDR_SHARD_BY_DEPTH=0: reach count only."""
+    return T if os.environ.get("DDR_SHARD_BY_DEPTH", "1") != "0" else 0
+
+
 def setup_split(args, net, rank, world, dist, dev, T):
     """C5 at N > 1: the largest outlet basin routed by a group of ranks (ddr_amd.split) when it exceeds
     twice a rank's share, the other basins LPT-sharded over the remaining ranks.  A hand-shake
@@ -260,7 +271,8 @@ def setup_split(args, net, rank, world, dist, dev, T):
     whole-basin sharding (returns None; so does a plan without a split).  DDR_SPLIT_BASIN=0 disables, =force splits even at N = 2."""
     from ddr_amd.split import SplitBasin, block_edges, plan_block_ranks, plan_ranks, sub_network
 
-    plan = plan_ranks(net.n, net.rows, net.cols, world, force=os.environ.get("DDR_SPLIT_BASIN") == "force")
+    plan = plan_ranks(net.n, net.rows, net.cols, world, factor=split_factor(),
+                      force=os.environ.get("DDR_SPLIT_BASIN") == "force", steps=shard_steps(T))
     ids_r, sp = plan[rank]
     any_split = any(s is not None for _, s in plan)
     if not any_split:
@@ -442,15 +454,15 @@ def main():
     t_setup = time.perf_counter()
     net, x_const = global_network(args)
     args.reaches_total = net.n
-    # this rank's outlet basins (LPT by reach count, distributed.shard_network; all of them at N = 1)
-    n_loc, rows, cols, ids = shard_network(net.n, net.rows, net.cols, rank, world) if world > 1 else (
+    # this rank's outlet basins (LPT by reach count refined by depth, distributed.shard_network; all of them at N = 1)
+    n_loc, rows, cols, ids = shard_network(net.n, net.rows, net.cols, rank, world, steps=shard_steps(T)) if world > 1 else (
         net.n, net.rows, net.cols, np.arange(net.n))
     g, split = None, None
     if alone and os.environ.get("DDR_BENCH_SPLIT_PLAN") == "1":
         # prediction runs: a rank outside the split group, with the shard the split plan gives it
         from ddr_amd.split import plan_ranks, sub_network
 
-        ids_r, sp = plan_ranks(net.n, net.rows, net.cols, world)[rank]
+        ids_r, sp = plan_ranks(net.n, net.rows, net.cols, world, factor=split_factor(), steps=shard_steps(T))[rank]
         if sp is not None:
             raise SystemExit("a split-group rank cannot run alone (its blocks wait for its peers)")
         n_loc, rows, cols, ids = sub_network(net.n, net.rows, net.cols, ids_r)

@@ -1822,32 +1822,19 @@ __global__ void nan_last_row_kernel(RouteArgs a) {
 // (a workgroup per tile re-read them: 12 B per reach per tile, a third of the q' bytes at G = 8), and the
 // next tile's q' loads are in flight while the current tile leaves LDS for the schedule rows.  A chunk's
 // tiles run on one CU back to back, so a tick row's segments written by consecutive tiles meet in its L2.
-#ifndef DDR_GX_XCD
-#define DDR_GX_XCD 0
-#endif
-#ifndef DDR_GX_TILES
-#define DDR_GX_TILES 4
-#endif
 template <typename R, int G, int BS, int KG>
 __global__ void __launch_bounds__(BS) gather_qprime_kernel(RouteArgs a, int chunk, int nchunks) {
   extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
   R* tile = reinterpret_cast<R*>(gsm);  // [G][nloc]
-  // workgroup -> (block, chunk): the dispatcher deals consecutive workgroup ids to the eight XCDs in turn, so
-  // XCD x receives ids x, x + 8, ...; those are mapped to the x-th eighth of the (chunk-major) work list -- one
-  // XCD works through a range of chunks of every block, so blocks whose reference ranges share q' lines read
-  // them through the same L2 at about the same time, and the two chunks that write a tick row's line meet there
-  const unsigned nwg = gridDim.x, id = blockIdx.x;
-  unsigned L = id;
-  if (DDR_GX_XCD && nwg >= 64) {
-    const unsigned per = nwg / 8, x = id % 8, i = id / 8;
-    L = i < per ? x * per + i : 8 * per + (id - 8 * per);  // (the tail nwg % 8 ids keep their own order)
-  }
-  const int nbk = (int)(nwg / (unsigned)nchunks);
-  const int bk = (int)(L % (unsigned)nbk);
+  // one-dimensional grid, chunk-major: the dispatcher starts every block's first chunk before any second one
+  // (mapping a contiguous eighth of this list to each XCD, so that blocks sharing q' lines read them through one
+  // L2, measured 2.7 % slower: profiles/r06/ab_r06.txt)
+  const int nbk = (int)(gridDim.x / (unsigned)nchunks);
+  const int bk = (int)(blockIdx.x % (unsigned)nbk);
   if (a.owned && !a.owned[bk]) return;  // split basin: another rank's block
   const BlockDesc B = a.s.blocks[bk];
   const int64_t T = a.T, N = a.N;
-  const int64_t tA = (int64_t)(L / (unsigned)nbk) * chunk;
+  const int64_t tA = (int64_t)(blockIdx.x / (unsigned)nbk) * chunk;
   if (tA >= T) return;
   const int64_t tB = tA + chunk < T ? tA + chunk : T;
   const int nl = B.nloc;
@@ -2335,7 +2322,7 @@ hipError_t launch_gather_qprime(const Graph* g, RouteArgs& a, hipStream_t stream
     const size_t sm = (size_t)gsteps * g->max_nloc * sizeof(R);
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     if (e != hipSuccess) return e;
-    constexpr int64_t kTilesPerChunk = DDR_GX_TILES;  // C5: 13.35 ms (2: 13.34, 8: 13.45, 16: 13.73; r05's tile per workgroup 13.92)
+    constexpr int64_t kTilesPerChunk = 4;  // C5: 13.35 ms (2: 13.34, 8: 13.45, 16: 13.73; r05's tile per workgroup 13.92)
     const int64_t nb = (int64_t)g->blocks.size();
     const int64_t chunk = kTilesPerChunk * gsteps;
     const int64_t y = (a.T + chunk - 1) / chunk;

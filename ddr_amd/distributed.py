@@ -13,7 +13,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .partition import basin_labels, extract_basins, shard_basins
+from .partition import basin_depths, basin_labels, extract_basins, shard_basins
 
 
 def rank_world():
@@ -24,16 +24,23 @@ def rank_world():
     return 0, 1
 
 
-def shard_network(n: int, rows: np.ndarray, cols: np.ndarray, rank: int, world: int):
-    """This rank's sub-network: whole outlet basins, LPT-balanced by reach count.
+def shard_network(n: int, rows: np.ndarray, cols: np.ndarray, rank: int, world: int, steps: int = 0):
+    """This rank's sub-network: whole outlet basins, LPT-balanced by reach count (``steps`` > 0: then refined
+    against the rank time model (T + deepest basin) x reach count, partition.shard_basins).
 
     Returns (n_sub, rows_sub, cols_sub, reach_ids) with ``reach_ids`` the global reach index of each
     local reach (topological order preserved).
     """
-    lab = basin_labels(n, rows, cols)
-    outlets, inv, sizes = np.unique(lab, return_inverse=True, return_counts=True)
+    if steps > 0:
+        lab, dep = basin_depths(n, rows, cols)
+        outlets, first, inv, sizes = np.unique(lab, return_index=True, return_inverse=True, return_counts=True)
+        shards = shard_basins(sizes, world, dep[first], steps)
+    else:
+        lab = basin_labels(n, rows, cols)
+        outlets, inv, sizes = np.unique(lab, return_inverse=True, return_counts=True)
+        shards = shard_basins(sizes, world)
     owner = np.empty(len(outlets), dtype=np.int64)
-    for r, idx in enumerate(shard_basins(sizes, world)):
+    for r, idx in enumerate(shards):
         owner[idx] = r
     keep = owner[inv] == rank
     return extract_basins(n, rows, cols, keep)

@@ -21,7 +21,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .partition import basin_labels, extract_basins, shard_basins
+from .partition import basin_depths, basin_labels, extract_basins, shard_basins
 
 
 def plan_block_ranks(nloc, k: int, prod=None, cons=None, tol: float = 0.05, sweeps: int = 8) -> np.ndarray:
@@ -112,15 +112,20 @@ def block_edges(graph):
     return nloc, prod[:info.n_cut], cons[:info.n_cut]
 
 
-def plan_ranks(n: int, rows, cols, world: int, factor: float = 2.0, force: bool = False):
+def plan_ranks(n: int, rows, cols, world: int, factor: float = 1.2, force: bool = False, steps: int = 0):
     """Per rank: (reach_ids, split) where split is None (whole basins, LPT over the ranks outside the
     split group) or (group_ranks, index_in_group) for the ranks that route the largest basin together.
 
     The largest basin is split when it exceeds ``factor`` x the per-rank mean (or ``force``) and at
-    least one rank remains for the other basins; its group has k = round(size / mean) ranks.  ``force``
-    with two ranks (a rehearsal) splits the largest basin over both and leaves the other basins out."""
-    lab = basin_labels(n, rows, cols)
-    outlets, inv, sizes = np.unique(lab, return_inverse=True, return_counts=True)
+    least one rank remains for the other basins; its group has k = round(size / mean) ranks (at least 2).
+    ``force`` with two ranks (a rehearsal) splits the largest basin over both and leaves the other basins out.
+    factor 1.2: C5 at N = 4 (the 281k-reach basin is 1.4 x a rank's share) splits it over two ranks -- the
+    basin alone on one rank took 55.5 ms, the two other ranks' 259k-reach shards 48.5-48.8 ms and the group
+    (its 511 workgroups routed alone: 66.3 ms) about half that (profiles/r06/n4_plan.txt).
+    ``steps`` > 0: whole basins are assigned by distributed.shard_network's depth-aware refinement."""
+    lab, dep = basin_depths(n, rows, cols)
+    outlets, first, inv, sizes = np.unique(lab, return_index=True, return_inverse=True, return_counts=True)
+    bdep = dep[first] if steps > 0 else None
     mean = n / max(world, 1)
     big = int(np.argmax(sizes))
     k = int(round(sizes[big] / mean)) if world > 1 else 0
@@ -129,7 +134,7 @@ def plan_ranks(n: int, rows, cols, world: int, factor: float = 2.0, force: bool 
     out = []
     if not split:
         owner = np.empty(len(outlets), dtype=np.int64)
-        for r, idx in enumerate(shard_basins(sizes, world)):
+        for r, idx in enumerate(shard_basins(sizes, world, bdep, steps)):
             owner[idx] = r
         for r in range(world):
             out.append((np.nonzero(owner[inv] == r)[0], None))
@@ -140,7 +145,7 @@ def plan_ranks(n: int, rows, cols, world: int, factor: float = 2.0, force: bool 
     others = world - k
     owner = np.full(len(outlets), -1, dtype=np.int64)
     if others > 0 and rest:  # (none left: a forced 2-rank rehearsal routes only the split basin)
-        for j, idx in enumerate(shard_basins(sizes[rest], others)):
+        for j, idx in enumerate(shard_basins(sizes[rest], others, None if bdep is None else bdep[rest], steps)):
             owner[np.asarray(rest)[idx]] = k + j
     for r in range(world):
         if r < k:

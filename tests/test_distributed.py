@@ -249,3 +249,30 @@ def test_two_rank_c3_objective_allreduce_and_gather():
         np.testing.assert_allclose(g, full_grad, rtol=2e-4, atol=1e-6)
         assert abs(loss - full_loss) <= 1e-9 * abs(full_loss)
         np.testing.assert_allclose(daily, full_daily, rtol=1e-8)  # SciPy solves of sub- vs whole network
+
+
+def test_basin_depths_and_depth_aware_shards():
+    """partition.basin_depths against a per-reach walk to the outlet; the depth-aware refinement of the LPT
+    shards lowers the modelled slowest rank, (T + deepest basin) x reaches, and still covers every basin once."""
+    from ddr_amd import synthetic
+    from ddr_amd.partition import basin_depths, basin_labels, shard_basins
+
+    net = synthetic.forest(synthetic.zipf_sizes(30000, 120, 0.3), seed=7, single_inflow=0.3)
+    lab, dep = basin_depths(net.n, net.rows, net.cols)
+    np.testing.assert_array_equal(lab, basin_labels(net.n, net.rows, net.cols))
+    down = np.full(net.n, -1)
+    down[net.cols] = net.rows
+    dist = np.zeros(net.n, dtype=np.int64)
+    for i in range(net.n - 1, -1, -1):  # rows > cols: a reach's downstream has the larger index
+        dist[i] = 0 if down[i] < 0 else dist[down[i]] + 1
+    ref = np.zeros(net.n, dtype=np.int64)
+    np.maximum.at(ref, lab, dist + 1)
+    np.testing.assert_array_equal(dep, ref[lab])
+    outlets, first, inv, sizes = np.unique(lab, return_index=True, return_inverse=True, return_counts=True)
+    bd = dep[first]
+    T = 720
+    for world in (2, 3, 4):
+        model = lambda sh: max((T + bd[i].max()) * sizes[i].sum() for i in sh)  # noqa: E731
+        plain, deep = shard_basins(sizes, world), shard_basins(sizes, world, bd, T)
+        assert model(deep) <= model(plain)
+        np.testing.assert_array_equal(np.sort(np.concatenate(deep)), np.arange(len(sizes)))
