@@ -7,7 +7,7 @@ if [ "$1" = "--json" ]; then
   HASH=$(python3 -c "import sys; sys.path.insert(0, '$R'); from ddr_amd import _lib; print(_lib.load().ddr_version().decode().split()[-1])")
   for wl in ${WLS:-c5 c3 c4 c2}; do
     python3 $R/tools/pmc_to_json.py $R/gpurun_out/$TAG/$wl $wl $HASH \
-      $(python3 -c "print({'c5':'8760 800000','c3':'2136 896201','c4':'8760 350000','c2':'8760 5000'}['$wl'])") profiles/r05/pmc_$wl || exit 1
+      $(python3 -c "print({'c5':'8760 800000','c3':'2136 896201','c4':'8760 350000','c2':'8760 5000'}['$wl'])") profiles/r06/pmc_$wl || exit 1
   done
   exit 0
 fi
