@@ -26,6 +26,7 @@ pytestmark = pytest.mark.gpu
 
 RANGES = {"n": [0.015, 0.25], "q_spatial": [0.0, 1.0], "p_spatial": [1.0, 200.0]}
 BAR = 1e-5
+MAXREL_BAR = 1e-4
 
 
 def _reaches(u, attrs):
@@ -56,7 +57,20 @@ def _check(res, bw, keys, bar):
     errs = {k: normrel(res[k], bw[k]) for k in keys}
     for k, e in errs.items():
         assert e <= bar, (k, errs)
+    # element-wise: north_star's max-rel bar (1e-4 for an fp32 result) over the elements above 1e-3 of the
+    # gradient's largest magnitude (smaller ones carry the fp32 cancellation of their own sums)
+    mx = {k: maxrel_above(res[k], bw[k], 1e-3) for k in keys}
+    print("normrel", errs, "maxrel", mx)
+    for k, e in mx.items():
+        assert e <= MAXREL_BAR, (k, mx)
     return errs
+
+
+def maxrel_above(a, b, frac):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    m = np.abs(b) >= frac * np.abs(b).max()
+    return float(np.max(np.abs(a[m] - b[m]) / np.abs(b[m]))) if m.any() else 0.0
 
 
 def test_exact_adjoint_on_the_deep_basin(cuda):
