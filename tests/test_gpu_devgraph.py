@@ -160,6 +160,16 @@ def test_device_collate_equals_host_collate(cuda):
         inside[x] = False
         ups = np.flatnonzero(inside)
         big.append((down[ups].astype(np.int32), ups.astype(np.int32), int(x)))
+    # pinned directly as well: the device union of the reference batch against the reference's own arrays
+    # (builders.py:55-109, merit.py:197-238), not only through the host union
+    d0 = collate_gauges_device(int(gold["n_conus"]), keep, cuda).to_host()
+    np.testing.assert_array_equal(d0.active, gold["ref_divide_ids"] - 500000)
+    np.testing.assert_array_equal(d0.crow, gold["ref_crow"])
+    np.testing.assert_array_equal(d0.col, gold["ref_col"])
+    assert d0.gage_compressed_indices == np.searchsorted(d0.active, gold["ref_gage_idx"]).tolist()
+    roff = gold["ref_outflow_off"]
+    for g_, o in enumerate(d0.outflow_idx):
+        np.testing.assert_array_equal(o, np.sort(gold["ref_outflow_flat"][roff[g_]:roff[g_ + 1]]))
     for n_conus, ss in ((int(gold["n_conus"]), keep), (net.n, big)):
         h = collate_gauges(n_conus, ss)
         d = collate_gauges_device(n_conus, ss, cuda).to_host()
