@@ -75,26 +75,31 @@ def shard_basins(sizes, n_ranks: int, depths=None, steps: int = 0) -> list[np.nd
     owner = lpt_assign(sizes, n_ranks, depths)
     if depths is not None and steps > 0 and n_ranks > 1 and len(sizes) > n_ranks:
         depths = np.asarray(depths, dtype=np.int64)
+        load = np.bincount(owner, weights=sizes, minlength=n_ranks).astype(np.float64)
 
-        def cost(r, extra=None, drop=None):
-            m = owner == r
-            if drop is not None:
-                m[drop] = False
-            load = float(sizes[m].sum()) + (0.0 if extra is None else float(sizes[extra]))
-            d = max(int(depths[m].max()) if m.any() else 0, 0 if extra is None else int(depths[extra]))
-            return (steps + d) * load
+        def deepest(r):
+            d = depths[owner == r]
+            return int(d.max()) if d.size else 0
 
-        for _ in range(4 * len(sizes)):
-            c = np.array([cost(r) for r in range(n_ranks)])
+        for _ in range(256):  # (a handful of moves in practice; bounded)
+            dmax = np.array([deepest(r) for r in range(n_ranks)], dtype=np.float64)
+            c = (steps + dmax) * load
             src, dst = int(np.argmax(c)), int(np.argmin(c))
-            best, bi = c[src], -1
-            for i in np.nonzero(owner == src)[0]:
-                m = max(cost(src, drop=i), cost(dst, extra=i))
-                if m < best:
-                    best, bi = m, int(i)
-            if bi < 0 or best > 0.99 * c[src]:
+            cand = np.nonzero(owner == src)[0]
+            d_src = depths[cand]
+            # the source rank's deepest basin once candidate i has left it
+            top = d_src.max()
+            second = np.sort(d_src)[-2] if len(d_src) > 1 else 0
+            left_d = np.where((d_src == top) & (np.count_nonzero(d_src == top) == 1), second, top)
+            c_src = (steps + left_d) * (load[src] - sizes[cand])
+            c_dst = (steps + np.maximum(dmax[dst], d_src)) * (load[dst] + sizes[cand])
+            m = np.maximum(c_src, c_dst)
+            j = int(np.argmin(m))
+            if m[j] > 0.99 * c[src]:
                 break
-            owner[bi] = dst
+            owner[cand[j]] = dst
+            load[src] -= sizes[cand[j]]
+            load[dst] += sizes[cand[j]]
     return [np.nonzero(owner == r)[0] for r in range(n_ranks)]
 
 
