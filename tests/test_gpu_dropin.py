@@ -167,6 +167,40 @@ def test_setup_inputs_semantics(cuda):
         MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda).forward()
 
 
+def test_flow_scale_semantics_and_chaos(cuda):
+    """tests/routing/test_flow_scaling.py:17-81: flow_scale None leaves q' as given; a 0.5 scale halves its own
+    segment only; a near-zero fraction (0.005) keeps q' and the routed discharge finite -- and the routed
+    discharge is that of the pre-scaled streamflow, bit for bit."""
+    n, T = 10, 24
+    hf = chain_dataclass(n, cuda, seed=4)
+    g = torch.Generator().manual_seed(4)
+    sf = torch.rand(T, n, generator=g) + 0.1
+    params = {"n": torch.rand(n, generator=g), "q_spatial": torch.rand(n, generator=g)}
+    mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    assert hf.flow_scale is None
+    mc.setup_inputs(hf, sf, params)
+    torch.testing.assert_close(mc.q_prime.cpu(), sf, rtol=0, atol=0)
+    fs = torch.ones(n)
+    fs[2] = 0.5
+    hf.flow_scale = fs
+    mc.setup_inputs(hf, sf, params)
+    torch.testing.assert_close(mc.q_prime[:, 2].cpu(), sf[:, 2] * 0.5)
+    keep = [i for i in range(n) if i != 2]
+    torch.testing.assert_close(mc.q_prime[:, keep].cpu(), sf[:, keep], rtol=0, atol=0)
+    fs = torch.ones(n)
+    fs[1] = 0.005
+    hf.flow_scale = fs
+    mc.setup_inputs(hf, sf, params)
+    assert torch.isfinite(mc.q_prime).all()
+    torch.testing.assert_close(mc.q_prime[:, 1].cpu(), sf[:, 1] * 0.005)
+    out = mc.forward()
+    assert out.shape == (1, T) and torch.isfinite(out).all()
+    hf.flow_scale = None
+    ref = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    ref.setup_inputs(hf, sf * fs.unsqueeze(0), params)
+    torch.testing.assert_close(out, ref.forward(), rtol=0, atol=0)
+
+
 def test_route_timestep_matches_forward_step(cuda):
     case, _ = golden_case("tree300", PARAMS_DEFAULT)
     mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
