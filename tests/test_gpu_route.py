@@ -339,3 +339,33 @@ def test_host_only_graph_is_refused_until_uploaded(cuda):
     res = run_hip(case, cuda, graph=g, grads=False)
     ref = O.route(case.network(), res["reaches"], case.qprime, case.bounds, dtype=np.float32)
     assert maxrel(res["runoff"], ref["runoff"]) <= 1e-6
+
+
+@pytest.mark.parametrize("which", ["sandbox", "hack5k"])
+def test_downstream_accumulation_positive_flow_mass_balance(cuda, which):
+    """tests/benchmarks/test_ddr.py:13-91 (the reference's integration checks of DDR routing): after a 50-step
+    spin-up the outlet's mean discharge is at least every contributor's, every reach's mean discharge is
+    positive, and the outlet's total discharge equals the total lateral inflow within 5 %.  On the RAPID
+    Sandbox network of the golden fixture (its 80-hour q' repeated over 2000 h) and on a 5000-reach Hack
+    basin (synthetic q', 2000 h)."""
+    T = 2000
+    if which == "sandbox":
+        case, _ = golden_case("sandbox", PARAMS_MOCK)
+        case.qprime = np.tile(case.qprime, (T // case.qprime.shape[0] + 1, 1))[:T].copy()
+        case.W = np.ones((case.n, T), np.float32)
+    else:
+        case = synthetic_case(synthetic.hack_basin(5000, seed=8), T, 8)
+    res = run_hip(case, cuda, grads=False, math="faithful")
+    q = res["runoff"].astype(np.float64)
+    down = np.full(case.n, -1)
+    down[case.cols] = case.rows
+    outlet = int(np.flatnonzero(down < 0)[0])
+    assert np.count_nonzero(down < 0) == 1
+    spin = 50
+    mean = q[:, spin:].mean(axis=1)
+    assert np.all(mean > 0)
+    for j in np.flatnonzero(down == outlet):
+        assert mean[outlet] >= mean[j]
+    total_in = float(case.qprime.astype(np.float64).sum())
+    total_out = float(q[outlet].sum())
+    assert abs(total_out - total_in) / total_in < 0.05, (total_in, total_out)
