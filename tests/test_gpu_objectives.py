@@ -198,3 +198,33 @@ def test_geometry_statistics_long_window(cuda, D):
         # hundreds of days (as test_c4_full_size_sampled_basins); min / max / median exact
         tol = 5e-6 if k.endswith("_mean") else 0.0
         assert maxrel(v[ok], orc[k][ok]) <= tol, (D, k)
+
+
+def _uniform_params(n_reaches):
+    """tests/geometry/test_geometry_stats.py:9-16: uniform parameters for a small network."""
+    return {"n": torch.full((n_reaches,), 0.035), "p_spatial": torch.full((n_reaches,), 21.0),
+            "q_spatial": torch.full((n_reaches,), 0.5), "slope": torch.full((n_reaches,), 0.001)}
+
+
+GEO_VARS = ("depth", "top_width", "bottom_width", "side_slope", "hydraulic_radius", "discharge")
+
+
+def test_geometry_statistics_properties(cuda):
+    """The reference's property tests of compute_geometry_statistics (tests/geometry/test_geometry_stats.py:19-58):
+    min <= median, mean <= max; a constant discharge gives equal statistics; a reach with higher discharge every
+    day is deeper and wider; a custom depth lower bound is respected."""
+    q = np.random.default_rng(42).uniform(1.0, 500.0, (30, 10)).astype(np.float32)
+    r = compute_geometry_statistics(**_uniform_params(10), daily_accumulated_discharge=q)
+    for v in GEO_VARS:
+        assert (r[f"{v}_min"] <= r[f"{v}_median"] + 1e-6).all() and (r[f"{v}_median"] <= r[f"{v}_max"] + 1e-6).all()
+        assert (r[f"{v}_min"] <= r[f"{v}_mean"] + 1e-6).all() and (r[f"{v}_mean"] <= r[f"{v}_max"] + 1e-6).all()
+    r = compute_geometry_statistics(**_uniform_params(5), daily_accumulated_discharge=np.full((10, 5), 25.0, np.float32))
+    for v in GEO_VARS:
+        for s in ("max", "median", "mean"):
+            np.testing.assert_allclose(r[f"{v}_min"], r[f"{v}_{s}"], rtol=1e-5)
+    q = np.array([[1.0, 100.0], [2.0, 200.0], [3.0, 300.0]], np.float32)
+    r = compute_geometry_statistics(**_uniform_params(2), daily_accumulated_discharge=q)
+    assert r["depth_mean"][1] > r["depth_mean"][0] and r["top_width_mean"][1] > r["top_width_mean"][0]
+    r = compute_geometry_statistics(**_uniform_params(3), daily_accumulated_discharge=np.full((2, 3), 1e-8, np.float32),
+                                    attribute_minimums={"depth": 0.5, "bottom_width": 0.01})
+    assert (r["depth_min"] >= 0.5).all()
