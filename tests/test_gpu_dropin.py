@@ -201,6 +201,22 @@ def test_flow_scale_semantics_and_chaos(cuda):
     torch.testing.assert_close(out, ref.forward(), rtol=0, atol=0)
 
 
+def test_fill_op_and_pattern_mapper(cuda):
+    """tests/routing/test_mmc.py:163-181, 234-258: fill_op(v) = I + diag(v) N (mmc.py:561-574); the pattern
+    mapper exposes map / crow_indices / col_indices and the dense network indices."""
+    mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+    hf = chain_dataclass(3, cuda)
+    mc.setup_inputs(hf, torch.ones(12, 3) * 2.0, {"n": torch.rand(3), "q_spatial": torch.rand(3)})
+    v = torch.tensor([0.5, -0.3, 0.1])
+    res = mc.fill_op(v)
+    assert res.shape == (3, 3)
+    dense = res.to_dense().cpu() if res.layout != torch.strided else res.cpu()
+    torch.testing.assert_close(dense, torch.eye(3) + torch.diag(v) @ hf.adjacency_matrix)
+    mapper, rows, cols = mc.create_pattern_mapper()
+    assert all(hasattr(mapper, a) for a in ("map", "crow_indices", "col_indices"))
+    assert isinstance(rows, torch.Tensor) and isinstance(cols, torch.Tensor)
+
+
 def test_route_timestep_matches_forward_step(cuda):
     case, _ = golden_case("tree300", PARAMS_DEFAULT)
     mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
