@@ -217,6 +217,33 @@ def test_fill_op_and_pattern_mapper(cuda):
     assert isinstance(rows, torch.Tensor) and isinstance(cols, torch.Tensor)
 
 
+@pytest.mark.parametrize("n,T", [(5, 12), (10, 24), (8, 36), (64, 96)])
+def test_full_workflow_state_updates_and_reproducibility(cuda, n, T):
+    """tests/routing/test_mmc.py:389-512 with the real fused solve instead of the reference's mocked one: the
+    state before and after setup_inputs, progress info, a (1, T) finite gauge output, _discharge_t updated to the
+    window's last step (the gauge reach's discharge is the output's last column), and two instances on the same
+    inputs giving the same bits."""
+    hf = chain_dataclass(n, cuda, seed=n)
+    g = torch.Generator().manual_seed(n)
+    sf = torch.rand(T, n, generator=g) + 0.1
+    params = {"n": torch.rand(n, generator=g), "q_spatial": torch.rand(n, generator=g)}
+    outs = []
+    for _ in range(2):
+        mc = MuskingumCunge(cfg_of(PARAMS_MOCK), device=cuda)
+        assert mc.routing_dataclass is None and mc.n is None and mc.q_spatial is None
+        mc.setup_inputs(hf, sf, params)
+        assert mc.routing_dataclass is not None and mc.n is not None and mc._discharge_t is not None
+        mc.set_progress_info(2, 5)
+        assert mc.epoch == 2 and mc.mini_batch == 5
+        q0 = mc._discharge_t.clone()
+        out = mc.forward()
+        assert out.shape == (1, T) and torch.isfinite(out).all()
+        assert not torch.equal(mc._discharge_t, q0)
+        torch.testing.assert_close(mc._discharge_t[-1], out[0, -1], rtol=0, atol=0)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_route_timestep_matches_forward_step(cuda):
     case, _ = golden_case("tree300", PARAMS_DEFAULT)
     mc = MuskingumCunge(cfg_of(PARAMS_DEFAULT), device=cuda)
