@@ -369,3 +369,26 @@ def test_downstream_accumulation_positive_flow_mass_balance(cuda, which):
     total_in = float(case.qprime.astype(np.float64).sum())
     total_out = float(q[outlet].sum())
     assert abs(total_out - total_in) / total_in < 0.05, (total_in, total_out)
+
+
+@pytest.mark.parametrize("name,params", GOLDEN, ids=[g[0] for g in GOLDEN])
+def test_fp32_gradients_elementwise_vs_fp64_model(cuda, name, params):
+    """north_star's element-wise gradient bar for an fp32 result (max rel <= 1e-4), against the fp64 model (the
+    fp64 oracle's forward and adjoint), over the gradient elements above 1e-3 of the largest: the default fp32
+    adjoint on the reference's golden networks (measured 5e-6 / 5.2e-5 / 8.8e-5 for Sandbox / tree300 / C1;
+    tools/dbg/grad_elementwise.py)."""
+    case, _ = golden_case(name, params)
+    res = run_hip(case, cuda)
+    r32 = res["reaches"]
+    r64 = O.Reaches(*(np.asarray(v, np.float64) for v in (r32.n, r32.q, r32.p, r32.length, r32.slope, r32.x)))
+    net = case.network()
+    fw = O.route(net, r64, case.qprime.astype(np.float64), case.bounds, dtype=np.float64)
+    bw = O.route_backward(net, r64, case.qprime.astype(np.float64), fw["x"], case.W.astype(np.float64), case.bounds)
+    u64 = {k: (None if v is None else v.astype(np.float64)) for k, v in case.u.items()}
+    g = O.param_grads_from_unit(bw["n"], bw["q_spatial"], bw["p_spatial"], u64["n"], u64["q_spatial"],
+                                u64.get("p_spatial"), case.params["parameter_ranges"])
+    for k, v in g.items():
+        a = np.asarray(res[f"grad_{k}"], np.float64)
+        m = np.abs(v) >= 1e-3 * np.abs(v).max()
+        err = float(np.max(np.abs(a[m] - v[m]) / np.abs(v[m])))
+        assert err <= 1e-4, (k, err)
