@@ -402,6 +402,8 @@ def main():
     ap.add_argument("--block-profile", default="", help="write a per-workgroup launch profile (JSON) here")
     ap.add_argument("--grad-qprime", action="store_true",
                     help="C5: q' requires grad, so the backward is the state-gradient adjoint (dL/dq' too)")
+    ap.add_argument("--exact-adjoint", action="store_true",
+                    help="fp32 backward as the exact adjoint of the fp32 trajectory (route(exact_adjoint=True), opt-in)")
     ap.add_argument("--stream", type=int, default=0,
                     help="C3, 1 GPU: also time K training steps over K different batches (a new gauge-union "
                          "adjacency per step, graphs built ahead on host threads by GraphPrefetcher)")
@@ -511,7 +513,8 @@ def main():
             for t_ in (u_n, u_q, u_p, qprime):
                 t_.grad = None
             n, q, p = denorm(u_n, u_q, u_p)
-            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, math=args.math)
+            runoff, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, consts=consts, math=args.math,
+                                     exact_adjoint=args.exact_adjoint)
             runoff.backward(W)
 
     elif args.workload == "c3":
@@ -534,7 +537,7 @@ def main():
             opt.zero_grad(set_to_none=True)
             n, q, p = model(feats)
             daily, _, _, _ = route(g, qprime, n, q, p, length, slope, xs, gauges=gz, daily=window, consts=consts,
-                                   math=args.math, steps=T, qprime_hours=qp_hours)
+                                   math=args.math, steps=T, qprime_hours=qp_hours, exact_adjoint=args.exact_adjoint)
             # the global mean absolute error over all ranks' gauges (train.py:94-97): this rank's share
             loss = loss_fn(daily, obs, wd, 1.0 / (G_global * (window.D - wd)))
             loss.backward()
@@ -672,6 +675,7 @@ def main():
                                               "torch": "PyTorch MLP 10-128-128-128-3"}[args.pnet]
                                              if args.workload == "c3" else None),
                        "step_graph": graph_mode,
+                       "backward": "exact adjoint of the fp32 trajectory" if args.exact_adjoint else "default fp32 adjoint",
                        "step_tail": (("fused HIP daily L1 + clip/Adam (ddr_amd.train)" if args.tail == "fused" and args.pnet == "fused"
                                       else "PyTorch l1_loss + clip_grad_norm_ + fused Adam") if args.workload == "c3" else None),
                        "forward_math": {"exact": "exact (reference op order, correctly rounded pow)",
